@@ -1,0 +1,318 @@
+"""ctypes mirror of include/bdpt/bdpt.h plus thin Python helpers (plumbing for tests / bench).
+
+The product is libbdpt_amd.so (HIP kernels + C-ABI) and the C++ `pathtracer` CLI next to it;
+this module only marshals scene descriptions and frames across the C-ABI. It never falls back
+to a CPU path: if the shared library is missing, `load_library()` raises.
+
+Reference interfaces mirrored (see include/bdpt/bdpt.h for the full map):
+  BidirectionalPathTracer::raytrace_pixel  src/pathtracer/bidirection.cpp:503-542
+  RaytracedRenderer::raytrace_tile         src/pathtracer/raytraced_renderer.cpp:595-620
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbdpt_amd.so")
+
+BDPT_OK = 0
+BDPT_E_INVALID = -1
+BDPT_E_UNSUPPORTED = -2
+BDPT_E_DEVICE = -3
+BDPT_E_NOMEM = -4
+
+PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
+MAT_DIFFUSE, MAT_EMISSION, MAT_MIRROR, MAT_GLASS, MAT_REFRACTION, MAT_MICROFACET = range(6)
+LIGHT_AREA, LIGHT_POINT, LIGHT_OTHER = 0, 1, 2
+FRAME_SAMPLE, FRAME_EYE, FRAME_LIGHT = 0, 1, 2
+
+_MAT_NAMES = {"diffuse": MAT_DIFFUSE, "emission": MAT_EMISSION, "mirror": MAT_MIRROR,
+              "glass": MAT_GLASS, "refraction": MAT_REFRACTION, "microfacet": MAT_MICROFACET}
+
+
+class Material(C.Structure):
+    _fields_ = [("type", C.c_int32), ("a", C.c_double * 3), ("b", C.c_double * 3),
+                ("ior", C.c_double), ("roughness", C.c_double)]
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("radiance", C.c_double * 3), ("position", C.c_double * 3),
+                ("direction", C.c_double * 3), ("dim_x", C.c_double * 3),
+                ("dim_y", C.c_double * 3), ("area", C.c_double)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("c2w", C.c_double * 9), ("w2c", C.c_double * 9),
+                ("hfov_deg", C.c_double), ("vfov_deg", C.c_double), ("nclip", C.c_double),
+                ("fclip", C.c_double)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("nprim", C.c_int32), ("prim_type", C.POINTER(C.c_int32)),
+                ("prim_geom", C.POINTER(C.c_double)), ("prim_mat", C.POINTER(C.c_int32)),
+                ("nmat", C.c_int32), ("mats", C.POINTER(Material)),
+                ("nlight", C.c_int32), ("lights", C.POINTER(Light)), ("camera", Camera)]
+
+
+class Params(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
+                ("max_depth", C.c_int32), ("seed", C.c_uint64), ("samples_per_lane", C.c_int32),
+                ("device", C.c_int32), ("collect_stats", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+class Tile(C.Structure):
+    _fields_ = [("x0", C.c_int32), ("y0", C.c_int32), ("w", C.c_int32), ("h", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("closest_rays", C.c_uint64),
+                ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("sph_tests", C.c_uint64), ("hits", C.c_uint64),
+                ("last_kernel_ms", C.c_double), ("bvh_nodes", C.c_uint64),
+                ("bvh_depth", C.c_uint64)]
+
+
+class Scene:
+    """Owns numpy arrays backing a SceneDesc (keeps them alive while the desc is used)."""
+
+    def __init__(self, prim_type, prim_geom, prim_mat, mats, lights, camera: dict,
+                 width: int = 0, height: int = 0):
+        self.prim_type = np.ascontiguousarray(prim_type, dtype=np.int32)
+        self.prim_geom = np.ascontiguousarray(prim_geom, dtype=np.float64).reshape(-1, 18)
+        self.prim_mat = np.ascontiguousarray(prim_mat, dtype=np.int32)
+        self.mats = (Material * max(1, len(mats)))()
+        for i, m in enumerate(mats):
+            self.mats[i] = m
+        self.nmat = len(mats)
+        self.lights = (Light * max(1, len(lights)))()
+        for i, l in enumerate(lights):
+            self.lights[i] = l
+        self.nlight = len(lights)
+        self.camera = camera
+        self.width, self.height = width, height
+
+    @property
+    def nprim(self) -> int:
+        return int(self.prim_type.shape[0])
+
+    def desc(self) -> SceneDesc:
+        d = SceneDesc()
+        d.nprim = self.nprim
+        d.prim_type = self.prim_type.ctypes.data_as(C.POINTER(C.c_int32))
+        d.prim_geom = self.prim_geom.ctypes.data_as(C.POINTER(C.c_double))
+        d.prim_mat = self.prim_mat.ctypes.data_as(C.POINTER(C.c_int32))
+        d.nmat = self.nmat
+        d.mats = C.cast(self.mats, C.POINTER(Material))
+        d.nlight = self.nlight
+        d.lights = C.cast(self.lights, C.POINTER(Light))
+        cam = Camera()
+        c = self.camera
+        cam.pos[:] = c["pos"]
+        cam.c2w[:] = [v for col in c["c2w_cols"] for v in col]
+        cam.w2c[:] = [v for col in c["w2c_cols"] for v in col]
+        cam.hfov_deg, cam.vfov_deg = c["hFov"], c["vFov"]
+        cam.nclip, cam.fclip = c["nClip"], c["fClip"]
+        d.camera = cam
+        return d
+
+
+def scene_from_json(js) -> Scene:
+    """Scene from the JSON dump format (tests/golden/scenes/*.json, written by
+    oracle/_ref/ref_driver or by the C++ loader's --dump-scene)."""
+    if isinstance(js, (str, os.PathLike)):
+        with open(js) as f:
+            js = json.load(f)
+    tris, sphs = js["triangles"], js["spheres"]
+    order = js.get("prim_order")  # list of ["t", i] / ["s", i] in scene order, if present
+    if order is None:
+        order = [("t", i) for i in range(len(tris))] + [("s", i) for i in range(len(sphs))]
+    ptype, geom, pmat = [], [], []
+    for kind, i in order:
+        g = [0.0] * 18
+        if kind == "t":
+            t = tris[i]
+            g[:18] = [x for v in t[:6] for x in v]
+            ptype.append(PRIM_TRIANGLE)
+            pmat.append(t[6])
+        else:
+            s = sphs[i]
+            g[0:3] = s[0]
+            g[3] = s[1]
+            ptype.append(PRIM_SPHERE)
+            pmat.append(s[2])
+        geom.append(g)
+    mats = []
+    for m in js["materials"]:
+        M = Material()
+        M.type = _MAT_NAMES.get(m["type"], -1)
+        if m["type"] in ("diffuse", "mirror"):
+            M.a[:] = m["reflectance"]
+        elif m["type"] == "emission":
+            M.a[:] = m["radiance"]
+        elif m["type"] == "glass":
+            M.a[:] = m["reflectance"]
+            M.b[:] = m["transmittance"]
+            M.ior, M.roughness = m["ior"], m.get("roughness", 0.0)
+        elif m["type"] == "refraction":
+            M.b[:] = m["transmittance"]
+            M.ior, M.roughness = m["ior"], m.get("roughness", 0.0)
+        mats.append(M)
+    lights = []
+    for l in js["lights"]:
+        L = Light()
+        if l["type"] == "area":
+            L.type = LIGHT_AREA
+            L.radiance[:], L.position[:] = l["radiance"], l["position"]
+            L.direction[:], L.dim_x[:], L.dim_y[:] = l["direction"], l["dim_x"], l["dim_y"]
+            L.area = l["area"]
+        elif l["type"] == "point":
+            L.type = LIGHT_POINT
+            L.radiance[:], L.position[:] = l["radiance"], l["position"]
+        else:
+            L.type = LIGHT_OTHER
+        lights.append(L)
+    cam = js["camera"]
+    return Scene(ptype, geom, pmat, mats, lights, cam, cam.get("screenW", 0), cam.get("screenH", 0))
+
+
+def retarget_camera(scene: Scene, width: int, height: int) -> Scene:
+    """Camera::set_screen_size (camera.cpp:83-89): screenDist fixed, FOV follows the frame size
+    (the reference's FOV quirk)."""
+    import math
+    c = dict(scene.camera)
+    sd = c["screenDist"]
+    c["hFov"] = 2 * math.degrees(math.atan(float(width) / (2 * sd)))
+    c["vFov"] = 2 * math.degrees(math.atan(float(height) / (2 * sd)))
+    c["screenW"], c["screenH"] = width, height
+    out = Scene(scene.prim_type, scene.prim_geom, scene.prim_mat,
+                [scene.mats[i] for i in range(scene.nmat)],
+                [scene.lights[i] for i in range(scene.nlight)], c, width, height)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+_lib = None
+
+
+def load_library(path: Optional[str] = None) -> C.CDLL:
+    """Loads libbdpt_amd.so (the HIP product). Raises if it is missing — there is no fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libbdpt_amd.so not built ({p}); run __graft_entry__.build()")
+    lib = C.CDLL(p)
+    lib.bdpt_abi_version.restype = C.c_int
+    lib.bdpt_last_error.restype = C.c_char_p
+    lib.bdpt_create.argtypes = [C.POINTER(SceneDesc), C.POINTER(Params), C.POINTER(C.c_void_p)]
+    lib.bdpt_destroy.argtypes = [C.c_void_p]
+    lib.bdpt_destroy.restype = None
+    lib.bdpt_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    lib.bdpt_clear.argtypes = [C.c_void_p]
+    lib.bdpt_render.argtypes = [C.c_void_p, C.POINTER(Tile), C.c_int32, C.c_int32, C.c_int32]
+    lib.bdpt_sync.argtypes = [C.c_void_p]
+    lib.bdpt_read_frame.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_float)]
+    lib.bdpt_frame_device_ptr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bdpt_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    lib.bdpt_trace_rays.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_int32,
+                                    C.POINTER(C.c_float), C.POINTER(C.c_int32)]
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class BDPTError(RuntimeError):
+    pass
+
+
+def _check(rc: int, lib) -> None:
+    if rc != BDPT_OK:
+        msg = lib.bdpt_last_error()
+        raise BDPTError(f"bdpt error {rc}: {msg.decode() if msg else ''}")
+
+
+class BidirectionalPathTracer:
+    """Host-side mirror of the reference's PathTracer entry points over the C-ABI
+    (pathtracer.h:36-69; bidirection.h:51-92). One instance = one device context."""
+
+    def __init__(self, scene: Scene, width: int, height: int, spp: int, max_depth: int,
+                 seed: int = 5489, device: int = 0, samples_per_lane: int = 0,
+                 collect_stats: bool = False):
+        self.lib = load_library()
+        self.scene = scene
+        self.width, self.height, self.spp, self.max_depth = width, height, spp, max_depth
+        p = Params()
+        p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
+        p.seed, p.samples_per_lane, p.device = seed, samples_per_lane, device
+        p.collect_stats = 1 if collect_stats else 0
+        self._desc = scene.desc()
+        ctx = C.c_void_p()
+        _check(self.lib.bdpt_create(C.byref(self._desc), C.byref(p), C.byref(ctx)), self.lib)
+        self.ctx = ctx
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.bdpt_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int) -> None:
+        _check(self.lib.bdpt_set_stream(self.ctx, C.c_void_p(stream_handle)), self.lib)
+
+    def clear(self) -> None:
+        _check(self.lib.bdpt_clear(self.ctx), self.lib)
+
+    def raytrace_tiles(self, tiles: Sequence[tuple] = (), spp_begin: int = 0,
+                       spp_count: Optional[int] = None) -> None:
+        n = len(tiles)
+        arr = (Tile * max(1, n))()
+        for i, t in enumerate(tiles):
+            arr[i] = Tile(*t)
+        cnt = self.spp - spp_begin if spp_count is None else spp_count
+        _check(self.lib.bdpt_render(self.ctx, arr if n else None, n, spp_begin, cnt), self.lib)
+
+    def raytrace_tile(self, x0: int, y0: int, w: int, h: int) -> None:
+        self.raytrace_tiles([(x0, y0, w, h)])
+
+    def raytrace_pixel(self, x: int, y: int) -> None:
+        self.raytrace_tiles([(x, y, 1, 1)])
+
+    def sync(self) -> None:
+        _check(self.lib.bdpt_sync(self.ctx), self.lib)
+
+    def read_frame(self, which: int = FRAME_SAMPLE) -> np.ndarray:
+        out = np.empty((self.height, self.width, 3), dtype=np.float32)
+        _check(self.lib.bdpt_read_frame(self.ctx, which, out.ctypes.data_as(C.POINTER(C.c_float))),
+               self.lib)
+        return out
+
+    def frame_device_ptr(self, which: int = FRAME_SAMPLE) -> int:
+        p = C.c_void_p()
+        _check(self.lib.bdpt_frame_device_ptr(self.ctx, which, C.byref(p)), self.lib)
+        return int(p.value or 0)
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check(self.lib.bdpt_get_stats(self.ctx, C.byref(s)), self.lib)
+        return s
+
+    def trace_rays(self, rays: np.ndarray, any_hit: bool = False):
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        t = np.empty(n, dtype=np.float32)
+        prim = np.empty(n, dtype=np.int32)
+        _check(self.lib.bdpt_trace_rays(self.ctx, rays.ctypes.data_as(C.POINTER(C.c_float)), n,
+                                        1 if any_hit else 0, t.ctypes.data_as(C.POINTER(C.c_float)),
+                                        prim.ctypes.data_as(C.POINTER(C.c_int32))), self.lib)
+        return t, prim

@@ -1,0 +1,175 @@
+/* include/bdpt/bdpt.h — C-ABI of the MI355X-native BDPT hot path (libbdpt_amd.so).
+ *
+ * Drop-in boundary for the reference's per-pixel BDPT loop:
+ *   reference interface                          replaced by
+ *   PathTracer::set_frame_size   pathtracer.h:36  -> bdpt_create (frame size in bdpt_params)
+ *   PathTracer::clear            pathtracer.h:43  -> bdpt_clear
+ *   PathTracer::raytrace_pixel   pathtracer.h:69  -> bdpt_render over a 1x1 tile
+ *     (BidirectionalPathTracer::raytrace_pixel, src/pathtracer/bidirection.cpp:503-542)
+ *   RaytracedRenderer::raytrace_tile             -> bdpt_render over a list of tiles
+ *     (src/pathtracer/raytraced_renderer.cpp:595-620)
+ *   BidirectionalPathTracer::{sampleBuffer, eyeBuffer, lightBuffer}
+ *     (bidirection.h:81, pathtracer.h:90)         -> bdpt_read_frame (BDPT_FRAME_*)
+ *   RaytracedRenderer::set_scene / build_accel    -> bdpt_create (scene desc; the BVH is built
+ *     (raytraced_renderer.cpp:105-127,350-374)       inside, reference midpoint split, bvh.cpp:51-129)
+ *
+ * Plain C types only: no torch, no HIP types in any signature (a stream is passed as void*).
+ * Every call returns 0 (BDPT_OK) or a negative BDPT_E_* code; bdpt_last_error() gives the text.
+ * No C++ exception crosses this boundary. Unsupported features that the reference can only
+ * assert(0) on under BDPT (microfacet sample_pdf, advanced_bsdf.cpp:144-148; environment /
+ * directional / spot / sphere / mesh lights, light.cpp:25-51,168-194, environment_light.cpp:182-208)
+ * are rejected at bdpt_create with BDPT_E_UNSUPPORTED instead of aborting.
+ */
+#ifndef BDPT_AMD_BDPT_H
+#define BDPT_AMD_BDPT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BDPT_ABI_VERSION 1
+
+enum bdpt_status {
+  BDPT_OK = 0,
+  BDPT_E_INVALID = -1,      /* bad argument / malformed scene */
+  BDPT_E_UNSUPPORTED = -2,  /* feature the reference BDPT cannot run (see header comment) */
+  BDPT_E_DEVICE = -3,       /* HIP runtime error (no device, launch failure, ...) */
+  BDPT_E_NOMEM = -4
+};
+
+/* Primitive kinds (src/scene/triangle.h, src/scene/sphere.h). */
+enum bdpt_prim_type { BDPT_PRIM_TRIANGLE = 0, BDPT_PRIM_SPHERE = 1 };
+
+/* BSDF kinds (src/pathtracer/bsdf.h:117-306). */
+enum bdpt_mat_type {
+  BDPT_MAT_DIFFUSE = 0,     /* a = reflectance                                  bsdf.cpp:52-85   */
+  BDPT_MAT_EMISSION = 1,    /* a = radiance                                     bsdf.cpp:99-118  */
+  BDPT_MAT_MIRROR = 2,      /* a = reflectance                          advanced_bsdf.cpp:17-35   */
+  BDPT_MAT_GLASS = 3,       /* a = reflectance, b = transmittance, ior  advanced_bsdf.cpp:198-259 */
+  BDPT_MAT_REFRACTION = 4,  /* b = transmittance, ior                   advanced_bsdf.cpp:163-184 */
+  BDPT_MAT_MICROFACET = 5   /* rejected: sample_pdf asserts under BDPT  advanced_bsdf.cpp:144-148 */
+};
+
+/* Light kinds (src/scene/light.h). Only area and point lights have BDPT methods. */
+enum bdpt_light_type { BDPT_LIGHT_AREA = 0, BDPT_LIGHT_POINT = 1, BDPT_LIGHT_OTHER = 2 };
+
+typedef struct bdpt_material {
+  int32_t type;
+  double a[3];
+  double b[3];
+  double ior;
+  double roughness;
+} bdpt_material;
+
+typedef struct bdpt_light {
+  int32_t type;
+  double radiance[3];
+  double position[3];
+  double direction[3];  /* area: unit emitting normal                                */
+  double dim_x[3];      /* area: rectangle edge vectors (light.cpp:199-203)          */
+  double dim_y[3];
+  double area;          /* |dim_x| * |dim_y|                                         */
+} bdpt_light;
+
+/* Pinhole camera state after Camera::configure/place/set_screen_size (camera.cpp:29-147). */
+typedef struct bdpt_camera {
+  double pos[3];
+  double c2w[9];        /* column-major: c2w[3*col + row] (CGL Matrix3x3 columns)     */
+  double w2c[9];        /* = c2w.inv() as the reference computes it                    */
+  double hfov_deg;
+  double vfov_deg;
+  double nclip;
+  double fclip;
+} bdpt_camera;
+
+/* Scene in the reference's primitive order (objects in scene order, faces in mesh order:
+ * RaytracedRenderer::build_accel, raytraced_renderer.cpp:350-374). The BVH is built from it. */
+typedef struct bdpt_scene_desc {
+  int32_t nprim;
+  const int32_t* prim_type;   /* nprim, bdpt_prim_type                                   */
+  const double* prim_geom;    /* nprim*18: triangle p1,p2,p3,n1,n2,n3; sphere c[3],r,... */
+  const int32_t* prim_mat;    /* nprim, index into mats                                  */
+  int32_t nmat;
+  const bdpt_material* mats;
+  int32_t nlight;
+  const bdpt_light* lights;
+  bdpt_camera camera;
+} bdpt_scene_desc;
+
+/* Random-number semantics of the device path: Philox4x32-10 keyed by seed, counter
+ * (pixel = x + y*W, global sample index, block, 0xB1D1). See DESIGN.md §RNG. */
+typedef struct bdpt_params {
+  int32_t width;              /* frame size (PathTracer::set_frame_size)                 */
+  int32_t height;
+  int32_t spp;                /* ns_aa: the 1/ns_aa weight of every sample                */
+  int32_t max_depth;          /* max_ray_depth (-m)                                      */
+  uint64_t seed;
+  int32_t samples_per_lane;   /* 0 = auto                                                 */
+  int32_t device;             /* HIP device ordinal                                       */
+  int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
+  int32_t reserved[5];
+} bdpt_params;
+
+typedef struct bdpt_tile {
+  int32_t x0, y0, w, h;       /* clipped to the frame like raytrace_tile does            */
+} bdpt_tile;
+
+enum bdpt_frame { BDPT_FRAME_SAMPLE = 0, BDPT_FRAME_EYE = 1, BDPT_FRAME_LIGHT = 2 };
+
+typedef struct bdpt_stats {
+  uint64_t samples;           /* pixel-samples rendered since the last clear            */
+  uint64_t rays;              /* closest-hit + connection queries                        */
+  uint64_t closest_rays;      /* walk rays (closest hit)                                 */
+  uint64_t shadow_rays;       /* connection rays (any hit)                               */
+  uint64_t node_visits;       /* AABBs fetched                                            */
+  uint64_t tri_tests;
+  uint64_t sph_tests;
+  uint64_t hits;              /* closest-hit queries that hit (shading record fetched)   */
+  double last_kernel_ms;      /* duration of the last bdpt_render's kernels (hipEvents)  */
+  uint64_t bvh_nodes;
+  uint64_t bvh_depth;
+} bdpt_stats;
+
+int bdpt_abi_version(void);
+const char* bdpt_last_error(void);
+
+/* Builds the BVH, flattens it, deep-copies the scene to HBM. The caller may free its arrays
+ * after this returns. */
+int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** ctx_out);
+void bdpt_destroy(void* ctx);
+
+/* All later work is enqueued on `stream` (a hipStream_t; NULL = the ctx's own stream). */
+int bdpt_set_stream(void* ctx, void* stream);
+
+/* Zeroes the frame buffers and counters (PathTracer::clear / set_frame_size). Async. */
+int bdpt_clear(void* ctx);
+
+/* Renders global sample indices [spp_begin, spp_begin+spp_count) of every pixel of the tiles.
+ * Asynchronous on the ctx stream. ntiles == 0 or tiles == NULL means the whole frame. */
+int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_begin,
+                int32_t spp_count);
+
+int bdpt_sync(void* ctx);
+
+/* Copies a W*H*3 float frame (row 0 = bottom, as HDRImageBuffer) to host memory (sync). */
+int bdpt_read_frame(void* ctx, int32_t which, float* rgb);
+
+/* Device pointer of a frame (W*H*3 float) for in-HBM consumers (RCCL reduce). */
+int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr);
+
+int bdpt_get_stats(void* ctx, bdpt_stats* out);
+
+/* Test hook: closest-hit / any-hit queries for a batch of rays through the device BVH
+ * (BVHAccel::intersect, bvh.cpp:161-188). rays: n*8 floats {o.xyz, d.xyz, min_t, max_t};
+ * out_t[n] (INFINITY if no hit), out_prim[n] (reference primitive index or -1). Sync. */
+int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, float* out_t,
+                    int32_t* out_prim);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BDPT_AMD_BDPT_H */

@@ -1,0 +1,1302 @@
+// oracle/bdpt_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference's per-pixel BDPT loop (dongmingli-Ben/bidirectional-pathtracing,
+// src/pathtracer/bidirection.cpp and what it calls). It is the checker for the HIP path: only
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it. Nothing in the
+// product (bidirectional-pathtracing_amd/) links or calls this file.
+//
+// One template, three instantiations (see DESIGN.md §Parity chain):
+//   mode 0  REF_STREAM  fp64 + the reference's RNG streams (two per-TU std::mt19937(5489) engines,
+//                       util/random_util.h:10-22, plus glibc rand() for light choice,
+//                       sampler.h:25-28) + glibc libm, tiles in raster order (single thread).
+//                       Pinned bit-exactly against oracle/_ref (the reference itself) dumps in
+//                       tests/golden/.
+//   mode 1  COUNTER64   fp64 + libm, but uniforms from the counter RNG (Philox4x32-10) — the bridge
+//                       between the reference semantics and the fp32 device semantics.
+//   mode 2  COUNTER32   fp32 + counter RNG + the device's deterministic transcendentals
+//                       (sincos of 2*pi*u by polynomial, cos(acos z) = z, integer powers by
+//                       products) — the per-sample parity partner of the HIP kernel.
+// Every arithmetic expression below follows the reference's operation order (CGL Vector3D
+// semantics: v/c = v*(1/c), normalize = *= 1/norm, dot = (x*x'+y*y')+z*z', CGL/include/CGL/
+// vector3D.h) so that mode 0 reproduces the reference's fp64 bits. Build: -O2 -ffp-contract=off.
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <limits>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bdpt/bdpt.h"
+
+namespace orc {
+
+static const double PI_D = 3.14159265358979323;  // CGL/include/CGL/misc.h:11
+static const float EPS_F = 0.00001f;              // misc.h:13
+
+// ----------------------------------------------------------------------------------------------
+// CGL Vector3D semantics (vector3D.h)
+template <class R>
+struct V3 {
+  R x, y, z;
+  V3() : x(0), y(0), z(0) {}
+  V3(R a, R b, R c) : x(a), y(b), z(c) {}
+  explicit V3(R c) : x(c), y(c), z(c) {}
+  R& operator[](int i) { return (&x)[i]; }
+  const R& operator[](int i) const { return (&x)[i]; }
+  V3 operator-() const { return V3(-x, -y, -z); }
+  V3 operator+(const V3& v) const { return V3(x + v.x, y + v.y, z + v.z); }
+  V3 operator-(const V3& v) const { return V3(x - v.x, y - v.y, z - v.z); }
+  V3 operator*(const V3& v) const { return V3(x * v.x, y * v.y, z * v.z); }
+  V3 operator/(const V3& v) const { return V3(x / v.x, y / v.y, z / v.z); }
+  V3 operator*(R c) const { return V3(x * c, y * c, z * c); }
+  V3 operator/(R c) const {                       // vector3D.h: rc = 1/c; rc*x
+    const R rc = R(1) / c;
+    return V3(rc * x, rc * y, rc * z);
+  }
+  void operator+=(const V3& v) { x += v.x; y += v.y; z += v.z; }
+  void operator*=(R c) { x *= c; y *= c; z *= c; }
+  void operator/=(R c) { (*this) *= (R(1) / c); }
+  R norm2() const { return x * x + y * y + z * z; }
+  R norm() const { return std::sqrt(norm2()); }
+  V3 unit() const { R rn = R(1) / norm(); return (*this) * rn; }
+  void normalize() { (*this) /= norm(); }
+};
+template <class R> inline V3<R> operator*(R c, const V3<R>& v) { return V3<R>(c * v.x, c * v.y, c * v.z); }
+template <class R> inline R dot(const V3<R>& u, const V3<R>& v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+template <class R> inline V3<R> cross(const V3<R>& u, const V3<R>& v) {
+  return V3<R>(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+
+// Matrix3x3 with columns X,Y,Z = o2w (bsdf.cpp:21-41). o2w*v = v.x*X + v.y*Y + v.z*Z
+// (matrix3x3.cpp:110-114); w2o*v = o2w.T()*v = (dot(v,X), dot(v,Y), dot(v,Z)).
+template <class R>
+struct Frame {
+  V3<R> X, Y, Z;
+  V3<R> to_world(const V3<R>& v) const { return v.x * X + v.y * Y + v.z * Z; }
+  V3<R> to_local(const V3<R>& v) const {
+    return V3<R>(v.x * X.x + v.y * X.y + v.z * X.z, v.x * Y.x + v.y * Y.y + v.z * Y.z,
+                 v.x * Z.x + v.y * Z.y + v.z * Z.z);
+  }
+};
+
+// make_coord_space (bsdf.cpp:21-41)
+template <class R>
+Frame<R> make_coord_space(const V3<R>& n) {
+  V3<R> z(n.x, n.y, n.z);
+  V3<R> h = z;
+  if (std::fabs(h.x) <= std::fabs(h.y) && std::fabs(h.x) <= std::fabs(h.z))
+    h.x = 1.0;
+  else if (std::fabs(h.y) <= std::fabs(h.x) && std::fabs(h.y) <= std::fabs(h.z))
+    h.y = 1.0;
+  else
+    h.z = 1.0;
+  z.normalize();
+  V3<R> y = cross(h, z);
+  y.normalize();
+  V3<R> x = cross(z, y);
+  x.normalize();
+  return Frame<R>{x, y, z};
+}
+
+// ----------------------------------------------------------------------------------------------
+// Random numbers.
+// Philox4x32-10 (Salmon et al. 2011). Counter (pixel, sample, block, 0xB1D1), key (seed lo, hi).
+inline void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ ctr[1] ^ k0;
+    uint32_t n2 = hi0 ^ ctr[3] ^ k1;
+    ctr[0] = n0; ctr[1] = lo1; ctr[2] = n2; ctr[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+// u = ((x >> 8) + 0.5) * 2^-24 : exact in fp32, in (0,1).
+inline float u24(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+
+struct CounterStream {
+  uint32_t k0, k1, pix, smp, block;
+  uint32_t buf[4];
+  int idx;
+  void init(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); pix = pixel; smp = sample; block = 0; idx = 4;
+  }
+  float next() {
+    if (idx == 4) {
+      buf[0] = pix; buf[1] = smp; buf[2] = block++; buf[3] = 0xB1D1u;
+      philox4x32_10(buf, k0, k1);
+      idx = 0;
+    }
+    return u24(buf[idx++]);
+  }
+};
+
+// Reference streams: util/random_util.h:10-22 (per-TU static engine, default seed 5489;
+// rmax = 1/(max-min); U = clamp(x*rmax, 1e-7, 0.99999999)).
+struct RefStreams {
+  std::mt19937 S;   // sampler.cpp's engine (all Sampler2D/3D draws)
+  std::mt19937 G;   // advanced_bsdf.cpp's engine (GlassBSDF coin_flip)
+  double rmax = 1.0 / (double)(4294967295u);
+  static double clampd(double x) { return std::min(std::max(x, 0.0000001), 0.99999999); }
+  double uS() { return clampd(double(S()) * rmax); }
+  double uG() { return clampd(double(G()) * rmax); }
+};
+
+// ----------------------------------------------------------------------------------------------
+// Policies: arithmetic type + RNG source + transcendentals.
+struct PolicyRef {              // mode 0
+  typedef double R;
+  RefStreams* rs;
+  R uS() { return rs->uS(); }
+  R uG() { return rs->uG(); }
+  int rand_light(int n) { return 0 + std::rand() % (n - 1 - 0 + 1); }   // sampler.h:25-28
+  static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
+  static R cos_acos(R z) { return std::cos(std::acos(z)); }
+  static R pow2(R x) { return std::pow(x, 2); }
+  static R pow4(R x) { return std::pow(x, 4); }
+  static R pow5(R x) { return std::pow(x, 5); }
+  static R tan_half_fov(double fov_deg) { return std::tan(fov_deg * PI_D / 360); }
+};
+struct PolicyC64 {              // mode 1
+  typedef double R;
+  CounterStream* cs;
+  R uS() { return (double)cs->next(); }
+  R uG() { return (double)cs->next(); }
+  int rand_light(int n) { int k = (int)((double)cs->next() * n); return k < n ? k : n - 1; }
+  static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
+  static R cos_acos(R z) { return std::cos(std::acos(z)); }
+  static R pow2(R x) { return std::pow(x, 2); }
+  static R pow4(R x) { return std::pow(x, 4); }
+  static R pow5(R x) { return std::pow(x, 5); }
+  static R tan_half_fov(double fov_deg) { return std::tan(fov_deg * PI_D / 360); }
+};
+
+// Deterministic fp32 sin/cos of 2*pi*u, u in (0,1): quadrant reduction (exact by Sterbenz) and
+// Taylor polynomials to degree 9/10 in f = u - k/4, |f| <= 1/8. Same op order as the device.
+static inline void cos_sin_2pi_f32(float u, float* c, float* s) {
+  float t = u * 4.0f;
+  int k = (int)(t + 0.5f);                 // t >= 0
+  float f = u - (float)k * 0.25f;          // exact
+  float f2 = f * f;
+  // sin(2*pi*f) = f*(a1 + f2*(a3 + f2*(a5 + f2*(a7 + f2*a9))))
+  float sp = f * (6.2831854820251465f +
+                  f2 * (-41.34170150756836f +
+                        f2 * (81.6052474975586f + f2 * (-76.70585632324219f + f2 * 42.058692932128906f))));
+  // cos(2*pi*f) = 1 + f2*(b2 + f2*(b4 + f2*(b6 + f2*(b8 + f2*b10))))
+  float cp = 1.0f + f2 * (-19.739208221435547f +
+                          f2 * (64.93939208984375f +
+                                f2 * (-85.45681762695312f + f2 * (60.2446403503418f + f2 * -26.42625617980957f))));
+  switch (k & 3) {
+    case 0: *c = cp; *s = sp; break;
+    case 1: *c = -sp; *s = cp; break;
+    case 2: *c = -cp; *s = -sp; break;
+    default: *c = sp; *s = -cp; break;
+  }
+}
+
+struct PolicyC32 {              // mode 2
+  typedef float R;
+  CounterStream* cs;
+  R uS() { return cs->next(); }
+  R uG() { return cs->next(); }
+  int rand_light(int n) { int k = (int)(cs->next() * (float)n); return k < n ? k : n - 1; }
+  static void cos_sin_2pi(R xi, R* c, R* s) { cos_sin_2pi_f32(xi, c, s); }
+  static R cos_acos(R z) { return z; }
+  static R pow2(R x) { return x * x; }
+  static R pow4(R x) { R x2 = x * x; return x2 * x2; }
+  static R pow5(R x) { R x2 = x * x; R x4 = x2 * x2; return x4 * x; }
+  static R tan_half_fov(double fov_deg) { return (float)std::tan(fov_deg * PI_D / 360); }
+};
+
+// ----------------------------------------------------------------------------------------------
+// Scene in precision R.
+template <class R>
+struct BBoxT {            // bbox.h:19-136
+  V3<R> mx, mn;
+  BBoxT() : mx(-INFINITY, -INFINITY, -INFINITY), mn(INFINITY, INFINITY, INFINITY) {}
+  explicit BBoxT(const V3<R>& p) : mx(p), mn(p) {}
+  BBoxT(const V3<R>& a, const V3<R>& b) : mx(b), mn(a) {}
+  void expand(const BBoxT& b) {
+    mn.x = std::min(mn.x, b.mn.x); mn.y = std::min(mn.y, b.mn.y); mn.z = std::min(mn.z, b.mn.z);
+    mx.x = std::max(mx.x, b.mx.x); mx.y = std::max(mx.y, b.mx.y); mx.z = std::max(mx.z, b.mx.z);
+  }
+  void expand(const V3<R>& p) {
+    mn.x = std::min(mn.x, p.x); mn.y = std::min(mn.y, p.y); mn.z = std::min(mn.z, p.z);
+    mx.x = std::max(mx.x, p.x); mx.y = std::max(mx.y, p.y); mx.z = std::max(mx.z, p.z);
+  }
+  V3<R> centroid() const { return (mn + mx) / R(2); }
+};
+
+template <class R>
+struct Ray {               // ray.h:20-71 (min_t/max_t are mutable there)
+  V3<R> o, d;
+  R min_t, max_t;
+};
+
+template <class R>
+struct Prim {
+  int type;
+  V3<R> p1, p2, p3, n1, n2, n3;  // triangle
+  V3<R> c; R r, r2;              // sphere (sphere.h:23)
+  int mat;
+  BBoxT<R> bbox;
+};
+
+template <class R>
+struct Mat {
+  int type;
+  V3<R> a, b;
+  R ior;
+};
+
+template <class R>
+struct Light {
+  int type;
+  V3<R> radiance, position, direction, dim_x, dim_y;
+  R area;
+};
+
+struct BvhNode {
+  int l = -1, r = -1;      // children (-1: leaf)
+  int start = 0, end = 0;  // leaf range into leaf_prims
+};
+
+template <class R>
+struct Scene {
+  std::vector<Prim<R>> prims;
+  std::vector<Mat<R>> mats;
+  std::vector<Light<R>> lights;
+  std::vector<BvhNode> nodes;
+  std::vector<BBoxT<R>> node_box;  // box used by the traversal in precision R
+  std::vector<int> leaf_prims;     // prim indices in DFS leaf order
+  std::vector<int> dfs_rank;       // prim -> position in DFS leaf order
+  int root = 0;
+  int depth = 0;
+  // camera
+  V3<R> cam_pos;
+  V3<R> c2w[3], w2c[3];  // columns
+  double hfov_deg, vfov_deg;
+  R nclip, fclip;
+};
+
+// BVH build: construct_bvh (bvh.cpp:51-129) in fp64 on the reference's bboxes.
+struct BuildCtx {
+  const std::vector<BBoxT<double>>* pb;
+  std::vector<BvhNode>* nodes;
+  std::vector<BBoxT<double>>* boxes;
+  std::vector<int>* leaf_prims;
+  int depth;
+};
+static int construct_bvh(BuildCtx& B, std::vector<int> prims, int depth) {
+  const auto& pb = *B.pb;
+  B.depth = std::max(B.depth, depth);
+  if (prims.size() <= 4) {
+    BBoxT<double> bbox = pb[prims[0]];
+    for (int p : prims) bbox.expand(pb[p]);
+    int id = (int)B.nodes->size();
+    BvhNode n;
+    n.start = (int)B.leaf_prims->size();
+    for (int p : prims) B.leaf_prims->push_back(p);
+    n.end = (int)B.leaf_prims->size();
+    B.nodes->push_back(n);
+    B.boxes->push_back(bbox);
+    return id;
+  }
+  double x_max = 0, x_min = 0, y_max = 0, y_min = 0, z_max = 0, z_min = 0;
+  for (size_t i = 0; i < prims.size(); i++) {
+    V3<double> c = pb[prims[i]].centroid();
+    x_max = i == 0 ? c.x : std::max(x_max, c.x);
+    x_min = i == 0 ? c.x : std::min(x_min, c.x);
+    y_max = i == 0 ? c.y : std::max(y_max, c.y);
+    y_min = i == 0 ? c.y : std::min(y_min, c.y);
+    z_max = i == 0 ? c.z : std::max(z_max, c.z);
+    z_min = i == 0 ? c.z : std::min(z_min, c.z);
+  }
+  double ranges[3] = {x_max - x_min, y_max - y_min, z_max - z_min};
+  double mins[3] = {x_min, y_min, z_min};
+  double max_range = std::max(ranges[0], std::max(ranges[1], ranges[2]));
+  int axis;
+  for (axis = 0; axis < 3; axis++)
+    if (ranges[axis] == max_range) break;
+  if (!(max_range > 0) || axis == 3) return -1;  // reference asserts (bvh.cpp:94)
+  double midpoint = mins[axis] + ranges[axis] / 2;
+  std::vector<int> left, right;
+  for (int p : prims) {
+    if (pb[p].centroid()[axis] <= midpoint) left.push_back(p);
+    else right.push_back(p);
+  }
+  if (left.empty() || right.empty()) return -1;   // bvh.cpp:117-118
+  int id = (int)B.nodes->size();
+  B.nodes->push_back(BvhNode());
+  B.boxes->push_back(BBoxT<double>());
+  int l = construct_bvh(B, left, depth + 1);
+  int r = construct_bvh(B, right, depth + 1);
+  if (l < 0 || r < 0) return -1;
+  BBoxT<double> bb((*B.boxes)[l].mn, (*B.boxes)[l].mx);
+  bb.expand((*B.boxes)[r]);
+  (*B.nodes)[id].l = l;
+  (*B.nodes)[id].r = r;
+  (*B.boxes)[id] = bb;
+  return id;
+}
+
+static inline V3<double> v3d(const double* p) { return V3<double>(p[0], p[1], p[2]); }
+
+template <class R>
+static V3<R> cvt(const V3<double>& v) { return V3<R>((R)v.x, (R)v.y, (R)v.z); }
+
+// Conservative fp32 box: round outward and pad by 2^-16 of the larger of |extent| and |coord|.
+static float pad_down(double v, double ext) {
+  double m = std::max(std::fabs(v), ext) * (1.0 / 65536.0) + 1e-30;
+  float f = (float)(v - m);
+  if ((double)f > v - m) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+static float pad_up(double v, double ext) {
+  double m = std::max(std::fabs(v), ext) * (1.0 / 65536.0) + 1e-30;
+  float f = (float)(v + m);
+  if ((double)f < v + m) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+template <class R>
+static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) {
+  // Primitives (Triangle ctor triangle.cpp:9-21; Sphere sphere.h:23) in fp64, then precision R.
+  std::vector<BBoxT<double>> pb(d->nprim);
+  sc.prims.resize(d->nprim);
+  for (int i = 0; i < d->nprim; i++) {
+    const double* g = d->prim_geom + 18 * (size_t)i;
+    Prim<R>& P = sc.prims[i];
+    P.type = d->prim_type[i];
+    P.mat = d->prim_mat[i];
+    if (P.mat < 0 || P.mat >= d->nmat) { err = "bad material index"; return BDPT_E_INVALID; }
+    if (P.type == BDPT_PRIM_TRIANGLE) {
+      V3<double> p1 = v3d(g), p2 = v3d(g + 3), p3 = v3d(g + 6);
+      BBoxT<double> b(p1);
+      b.expand(p2);
+      b.expand(p3);
+      pb[i] = b;
+      P.p1 = cvt<R>(p1); P.p2 = cvt<R>(p2); P.p3 = cvt<R>(p3);
+      P.n1 = cvt<R>(v3d(g + 9)); P.n2 = cvt<R>(v3d(g + 12)); P.n3 = cvt<R>(v3d(g + 15));
+    } else if (P.type == BDPT_PRIM_SPHERE) {
+      V3<double> c = v3d(g);
+      double r = g[3];
+      pb[i] = BBoxT<double>(c - V3<double>(r, r, r), c + V3<double>(r, r, r));
+      P.c = cvt<R>(c);
+      P.r = (R)r;
+      P.r2 = (sizeof(R) == 8) ? (R)(r * r) : P.r * P.r;  // sphere.h:23 r2(r*r)
+    } else {
+      err = "bad primitive type";
+      return BDPT_E_INVALID;
+    }
+  }
+  for (int i = 0; i < d->nmat; i++) {
+    const bdpt_material& m = d->mats[i];
+    if (m.type == BDPT_MAT_MICROFACET || m.type < 0 || m.type > BDPT_MAT_MICROFACET) {
+      err = "unsupported material (microfacet sample_pdf asserts under BDPT)";
+      return BDPT_E_UNSUPPORTED;
+    }
+    Mat<R> M;
+    M.type = m.type;
+    M.a = cvt<R>(v3d(m.a));
+    M.b = cvt<R>(v3d(m.b));
+    M.ior = (R)m.ior;
+    sc.mats.push_back(M);
+  }
+  if (d->nlight < 1) { err = "scene has no light"; return BDPT_E_INVALID; }
+  for (int i = 0; i < d->nlight; i++) {
+    const bdpt_light& l = d->lights[i];
+    if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT) {
+      err = "unsupported light type under BDPT";
+      return BDPT_E_UNSUPPORTED;
+    }
+    Light<R> L;
+    L.type = l.type;
+    L.radiance = cvt<R>(v3d(l.radiance));
+    L.position = cvt<R>(v3d(l.position));
+    L.direction = cvt<R>(v3d(l.direction));
+    L.dim_x = cvt<R>(v3d(l.dim_x));
+    L.dim_y = cvt<R>(v3d(l.dim_y));
+    L.area = (R)l.area;
+    sc.lights.push_back(L);
+  }
+  // BVH (fp64 build, reference topology).
+  std::vector<BBoxT<double>> boxes;
+  BuildCtx B{&pb, &sc.nodes, &boxes, &sc.leaf_prims, 0};
+  std::vector<int> all(d->nprim);
+  for (int i = 0; i < d->nprim; i++) all[i] = i;
+  if (d->nprim == 0) { err = "empty scene"; return BDPT_E_INVALID; }
+  sc.root = construct_bvh(B, all, 0);
+  if (sc.root < 0) { err = "degenerate BVH split"; return BDPT_E_INVALID; }
+  sc.depth = B.depth;
+  sc.dfs_rank.assign(d->nprim, 0);
+  for (size_t i = 0; i < sc.leaf_prims.size(); i++) sc.dfs_rank[sc.leaf_prims[i]] = (int)i;
+  sc.node_box.resize(boxes.size());
+  for (size_t i = 0; i < boxes.size(); i++) {
+    if (sizeof(R) == 8) {
+      sc.node_box[i].mn = cvt<R>(boxes[i].mn);
+      sc.node_box[i].mx = cvt<R>(boxes[i].mx);
+    } else {
+      V3<double> e = boxes[i].mx - boxes[i].mn;
+      double ext = std::max(e.x, std::max(e.y, e.z));
+      for (int k = 0; k < 3; k++) {
+        sc.node_box[i].mn[k] = (R)pad_down(boxes[i].mn[k], ext);
+        sc.node_box[i].mx[k] = (R)pad_up(boxes[i].mx[k], ext);
+      }
+    }
+  }
+  // Camera
+  const bdpt_camera& c = d->camera;
+  sc.cam_pos = cvt<R>(v3d(c.pos));
+  for (int k = 0; k < 3; k++) {
+    sc.c2w[k] = cvt<R>(v3d(c.c2w + 3 * k));
+    sc.w2c[k] = cvt<R>(v3d(c.w2c + 3 * k));
+  }
+  sc.hfov_deg = c.hfov_deg;
+  sc.vfov_deg = c.vfov_deg;
+  sc.nclip = (R)c.nclip;
+  sc.fclip = (R)c.fclip;
+  return BDPT_OK;
+}
+
+// ----------------------------------------------------------------------------------------------
+struct Stats {
+  uint64_t rays = 0, closest = 0, shadow = 0, nodes = 0, tri = 0, sph = 0, hits = 0;
+};
+
+template <class P>
+struct Tracer {
+  typedef typename P::R R;
+  typedef V3<R> V;
+  const Scene<R>& sc;
+  P pol;
+  int max_depth, W, H, ns_aa;
+  R tanh_, tanv_;
+  Stats st;
+  // splat sink (lightBuffer & sampleBuffer updates, bidirection.cpp:457-466)
+  std::vector<double>* light_buf = nullptr;   // W*H*3
+  std::vector<double>* sample_buf = nullptr;  // mode 0 only (exact sampleBuffer order)
+
+  struct Isect {            // intersection.h:21-34
+    R t = (R)INFINITY;
+    int prim = -1;
+    V n;
+    int mat = -1;           // bsdf == NULL
+  };
+  struct Vertex {           // bidirection.h:29-46
+    Isect isect;
+    R p = 1, q = 1;
+    V alpha = V(1), position;
+    bool is_light = false, new_sample = false;
+    R dir_pdf = 0;
+  };
+
+  Tracer(const Scene<R>& s, P p, int md, int w, int h, int spp)
+      : sc(s), pol(p), max_depth(md), W(w), H(h), ns_aa(spp) {
+    tanh_ = P::tan_half_fov(sc.hfov_deg);
+    tanv_ = P::tan_half_fov(sc.vfov_deg);
+  }
+
+  // ---------------- geometry ----------------
+  // BBox::intersect (bbox.cpp:10-56): rejects only when tmax < tmin.
+  bool box_hit(const BBoxT<R>& b, const Ray<R>& r) const {
+    R tmin_x = (b.mn.x - r.o.x) / r.d.x, tmax_x = (b.mx.x - r.o.x) / r.d.x;
+    if (tmax_x < tmin_x) std::swap(tmin_x, tmax_x);
+    R tmin_y = (b.mn.y - r.o.y) / r.d.y, tmax_y = (b.mx.y - r.o.y) / r.d.y;
+    if (tmax_y < tmin_y) std::swap(tmin_y, tmax_y);
+    R tmin_z = (b.mn.z - r.o.z) / r.d.z, tmax_z = (b.mx.z - r.o.z) / r.d.z;
+    if (tmax_z < tmin_z) std::swap(tmin_z, tmax_z);
+    R tmin = std::max(tmin_x, std::max(tmin_y, tmin_z));
+    R tmax = std::min(tmax_x, std::min(tmax_y, tmax_z));
+    if (tmax < tmin) return false;
+    return true;
+  }
+  // Triangle::intersect (triangle.cpp:57-95)
+  bool tri_hit(const Prim<R>& T, Ray<R>& r, Isect* is, int idx) {
+    st.tri++;
+    V o = r.o, d = r.d, p0 = T.p1, p1 = T.p2, p2 = T.p3;
+    V e1 = p1 - p0, e2 = p2 - p0, s = o - p0;
+    V s1 = cross(d, e2), s2 = cross(s, e1);
+    R denom = dot(s1, e1);
+    R t = dot(s2, e2) / denom;
+    R b1 = dot(s1, s) / denom;
+    R b2 = dot(s2, d) / denom;
+    if (t >= r.min_t && t <= r.max_t && b1 >= 0 && b2 >= 0 && b1 + b2 <= 1) {
+      V normal = T.n1 * (1 - b1 - b2) + b1 * T.n2 + b2 * T.n3;
+      normal.normalize();
+      r.max_t = t;
+      is->t = t;
+      is->n = normal;
+      is->prim = idx;
+      is->mat = T.mat;
+      return true;
+    }
+    return false;
+  }
+  // Sphere::test/intersect (sphere.cpp:11-35,61-93)
+  bool sph_hit(const Prim<R>& S, Ray<R>& r, Isect* is, int idx) {
+    st.sph++;
+    V o = r.o, d = r.d, vc = S.c;
+    R a = d.norm2();
+    R b = 2 * dot(o - vc, d);
+    R c = (o - vc).norm2() - S.r2;
+    R delta = b * b - 4 * a * c;
+    if (delta < 0) return false;
+    R root = std::sqrt(delta);
+    R t1 = (-b - root) / (2 * a);
+    R t2 = (-b + root) / (2 * a);
+    R t = -1;
+    if (t1 >= r.min_t && t1 <= r.max_t) t = t1;
+    else if (t2 >= r.min_t && t2 <= r.max_t) t = t2;
+    if (t > 0) {
+      r.max_t = t;
+      V p = r.o + t * r.d;
+      V normal = p - S.c;
+      normal.normalize();
+      is->t = t;
+      is->n = normal;
+      is->prim = idx;
+      is->mat = S.mat;
+      return true;
+    }
+    return false;
+  }
+  // BVHAccel::intersect (bvh.cpp:161-188): visit every child whose slab test passes, l then r.
+  bool node_hit(Ray<R>& r, Isect* is, int node) {
+    st.nodes++;
+    if (!box_hit(sc.node_box[node], r)) return false;
+    const BvhNode& N = sc.nodes[node];
+    if (N.l < 0) {
+      bool hit = false, h;
+      for (int k = N.start; k < N.end; k++) {
+        int pi = sc.leaf_prims[k];
+        const Prim<R>& pr = sc.prims[pi];
+        h = (pr.type == BDPT_PRIM_TRIANGLE) ? tri_hit(pr, r, is, pi) : sph_hit(pr, r, is, pi);
+        hit = h || hit;
+      }
+      return hit;
+    }
+    bool h1 = node_hit(r, is, N.l);
+    bool h2 = node_hit(r, is, N.r);
+    return h1 || h2;
+  }
+  bool intersect(Ray<R> r, Isect* is, bool closest) {
+    st.rays++;
+    if (closest) st.closest++; else st.shadow++;
+    bool h = node_hit(r, is, sc.root);
+    if (h && closest) st.hits++;
+    return h;
+  }
+
+  // ---------------- samplers (sampler.cpp) ----------------
+  void grid2d(R* x, R* y) {        // Vector2D(random_uniform(), random_uniform()): y drawn first
+    R b = pol.uS();
+    R a = pol.uS();
+    *x = a;
+    *y = b;
+  }
+  V cosine_hemi(R* pdf) {          // sampler.cpp:76-86
+    R Xi1 = pol.uS();
+    R Xi2 = pol.uS();
+    R r = std::sqrt(Xi1);
+    *pdf = std::sqrt(1 - Xi1) / R(PI_D);
+    R c, s;
+    P::cos_sin_2pi(Xi2, &c, &s);
+    return V(r * c, r * s, std::sqrt(1 - Xi1));
+  }
+  static R cosine_pdf(const V& v) { return v.z > 0 ? v.z / R(PI_D) : R(0); }   // sampler.cpp:92-95
+  V sphere_uniform() {             // sampler.cpp:17-25
+    R z = pol.uS() * 2 - 1;
+    R sinTheta = std::sqrt(std::max(R(0), R(1.0f) - z * z));
+    R u = pol.uS();
+    R c, s;
+    P::cos_sin_2pi(u, &c, &s);
+    return V(c * sinTheta, s * sinTheta, z);
+  }
+
+  // ---------------- BSDFs ----------------
+  static void reflect(const V& wo, V* wi) { *wi = V(-wo.x, -wo.y, wo.z); }   // advanced_bsdf.cpp:272-277
+  static bool refract(const V& wo, V* wi, R ior) {                            // :279-303
+    bool enter = wo.z > 0;
+    R eta = enter ? R(1) / ior : ior;
+    R z_sq = 1 - eta * eta * (1 - wo.z * wo.z);
+    if (z_sq < 0) return false;
+    R sgn = enter ? R(-1) : R(1);
+    *wi = V(-eta * wo.x, -eta * wo.y, sgn * std::sqrt(z_sq));
+    return true;
+  }
+  V bsdf_f(int m, const V& wo, const V& wi) const {
+    const Mat<R>& M = sc.mats[m];
+    if (M.type == BDPT_MAT_DIFFUSE) {                                         // bsdf.cpp:52-62
+      if (wo.z < 0. || wi.z < 0.) return V();
+      return M.a / R(PI_D);
+    }
+    return V();                                      // emission/mirror/glass/refraction f = 0
+  }
+  V bsdf_sample_f(int m, const V& wo, V* wi, R* pdf) {
+    const Mat<R>& M = sc.mats[m];
+    switch (M.type) {
+      case BDPT_MAT_DIFFUSE: {                                                // bsdf.cpp:67-77
+        *wi = cosine_hemi(pdf);
+        return bsdf_f(m, wo, *wi);
+      }
+      case BDPT_MAT_EMISSION: {                                               // bsdf.cpp:103-108
+        *pdf = R(1.0) / R(PI_D);
+        *wi = cosine_hemi(pdf);
+        return V();
+      }
+      case BDPT_MAT_MIRROR: {                                                 // advanced_bsdf.cpp:21-29
+        reflect(wo, wi);
+        *pdf = 1;
+        R costheta = std::fabs(wi->z) / wi->norm();
+        return M.a / costheta;
+      }
+      case BDPT_MAT_REFRACTION: {                                             // :163-178
+        if (!refract(wo, wi, M.ior)) { *pdf = 1; return V(); }  // reference leaves pdf unset
+        *pdf = 1;
+        R eta = wo.z > 0 ? R(1) / M.ior : M.ior;
+        R costheta = std::fabs(wi->z) / wi->norm();
+        return M.b / costheta / (eta * eta);
+      }
+      default: {                                                              // glass :198-237
+        V wi_reflect, wi_refract;
+        reflect(wo, &wi_reflect);
+        bool tir = !refract(wo, &wi_refract, M.ior);
+        if (tir) {
+          *pdf = 1;
+          *wi = wi_reflect;
+          R costheta = std::fabs(wi->z) / wo.norm();
+          return M.a / costheta;
+        }
+        R c_ref = std::fabs(wi_refract.z) / wi_refract.norm();
+        R eta = wo.z > 0 ? R(1) / M.ior : M.ior;
+        R R0 = P::pow2((1 - eta) / (1 + eta));
+        R Rf = R0 + (1 - R0) * P::pow5(1 - c_ref);
+        if (pol.uG() < Rf) {                                                  // coin_flip(R)
+          *wi = wi_reflect;
+          *pdf = Rf;
+          R costheta = std::fabs(wi->z) / wi->norm();
+          return Rf * M.a / costheta;
+        } else {
+          *wi = wi_refract;
+          *pdf = 1 - Rf;
+          R costheta = std::fabs(wi->z) / wi->norm();
+          return (1 - Rf) * M.b / costheta / (eta * eta);
+        }
+      }
+    }
+  }
+  R bsdf_sample_pdf(int m, const V& wo, const V& wi) const {
+    const Mat<R>& M = sc.mats[m];
+    switch (M.type) {
+      case BDPT_MAT_DIFFUSE:
+      case BDPT_MAT_EMISSION: return cosine_pdf(wi);                           // bsdf.cpp:81-85,112-117
+      case BDPT_MAT_MIRROR:
+      case BDPT_MAT_REFRACTION: return 1.;                                     // advanced_bsdf.cpp:32,181
+      default: {                                                               // glass :240-259
+        V wo_reflect, wo_refract, wi_ = wi;
+        reflect(wi_, &wo_reflect);
+        bool tir = !refract(wi_, &wo_refract, M.ior);
+        if (tir) return 1.;
+        R c = std::fabs(wo_refract.z) / wo_refract.norm();
+        R eta = wo.z > 0 ? R(1) / M.ior : M.ior;
+        R R0 = P::pow2((1 - eta) / (1 + eta));
+        R Rf = R0 + (1 - R0) * P::pow5(1 - c);
+        if (wi.z > 0.) return Rf;
+        return 1 - Rf;
+      }
+    }
+  }
+  V get_emission(int m) const { return sc.mats[m].type == BDPT_MAT_EMISSION ? sc.mats[m].a : V(); }
+  bool is_delta(int m) const {
+    if (m < 0) return false;
+    int t = sc.mats[m].type;
+    return t == BDPT_MAT_MIRROR || t == BDPT_MAT_GLASS || t == BDPT_MAT_REFRACTION;
+  }
+
+  // ---------------- lights (light.cpp) ----------------
+  V light_sample_Le(const Light<R>& L, Ray<R>* ray, R* point_pdf, R* dir_pdf, V* normal) {
+    if (L.type == BDPT_LIGHT_POINT) {                                        // :115-123
+      V d = sphere_uniform();
+      ray->o = L.position; ray->d = d; ray->min_t = 0; ray->max_t = (R)INFINITY;
+      *point_pdf = 1;
+      *dir_pdf = R(0.25) / R(PI_D);
+      *normal = d;
+      return L.radiance;
+    }
+    R sx, sy;                                                                 // :219-232
+    grid2d(&sx, &sy);
+    sx = sx - R(0.5f);
+    sy = sy - R(0.5f);
+    V o = L.position + sx * L.dim_x + sy * L.dim_y;
+    V d = cosine_hemi(dir_pdf);
+    Frame<R> f = make_coord_space(L.direction);
+    ray->o = o; ray->d = f.to_world(d); ray->min_t = 0; ray->max_t = (R)INFINITY;
+    *point_pdf = R(1.) / L.area;
+    *normal = L.direction;
+    return L.radiance;
+  }
+  V light_sample_Le_point(const Light<R>& L, const V& p, V* wi, V* point, R* dist, R* point_pdf,
+                          R* dir_pdf, V* normal) {
+    if (L.type == BDPT_LIGHT_POINT) {                                        // :125-137
+      V d = L.position - p;
+      *wi = d.unit();
+      *dist = d.norm();
+      *point_pdf = 1.0;
+      *dir_pdf = R(0.25) / R(PI_D);
+      *normal = -(*wi);
+      *point = L.position;
+      return L.radiance;
+    }
+    R sx, sy;                                                                 // :234-255
+    grid2d(&sx, &sy);
+    sx = sx - R(0.5f);
+    sy = sy - R(0.5f);
+    *point = L.position + sx * L.dim_x + sy * L.dim_y;
+    V d = *point - p;
+    R cosTheta = dot(d, L.direction);
+    R sqDist = d.norm2();
+    R dd = std::sqrt(sqDist);
+    *wi = d / dd;
+    *dist = dd;
+    *point_pdf = R(1.) / L.area;
+    *normal = L.direction;
+    Frame<R> f = make_coord_space(L.direction);
+    *dir_pdf = cosine_pdf(f.to_local(-(*wi)));
+    return cosTheta < 0 ? L.radiance : V();
+  }
+  bool light_contain_point(const Light<R>& L, const V& p) const {
+    if (L.type == BDPT_LIGHT_POINT) return (p - L.position).norm() < R(EPS_F);   // :139-142
+    V d = L.position - p;                                                     // :257-262
+    d.normalize();
+    return std::fabs(dot(d, L.direction)) < R(EPS_F);
+  }
+  V light_sample_pdf(const Light<R>& L, const V& p, const V& wi, R* point_pdf, R* dir_pdf) const {
+    if (!light_contain_point(L, p)) { *point_pdf = 0.; *dir_pdf = 0.; return V(); }
+    if (L.type == BDPT_LIGHT_POINT) {                                        // :144-153
+      *point_pdf = 1.0;
+      *dir_pdf = R(0.25) / R(PI_D);
+      return L.radiance;
+    }
+    *point_pdf = R(1.) / L.area;                                              // :264-284
+    Frame<R> f = make_coord_space(L.direction);
+    V wl = f.to_local(-wi);
+    wl.normalize();
+    *dir_pdf = cosine_pdf(wl);
+    return *dir_pdf > 0. ? L.radiance : V();
+  }
+
+  // ---------------- camera (camera.cpp) ----------------
+  Ray<R> generate_ray(R x, R y) const {                                       // :191-212
+    V rd;
+    rd.x = (2 * x - 1) * tanh_;
+    rd.y = (2 * y - 1) * tanv_;
+    rd.z = -1;
+    V wd = rd.x * sc.c2w[0] + rd.y * sc.c2w[1] + rd.z * sc.c2w[2];
+    wd.normalize();
+    Ray<R> r;
+    r.o = sc.cam_pos;
+    r.d = wd;
+    r.min_t = sc.nclip;
+    r.max_t = sc.fclip;
+    return r;
+  }
+  V sample_ray_pdf(const V& p, V* wi, V* eye_point, R* dist, R* point_pdf, R* dir_pdf, V* normal,
+                   int* x, int* y) const {                                     // :214-248
+    *wi = sc.cam_pos - p;
+    *dist = wi->norm();
+    wi->normalize();
+    *eye_point = sc.cam_pos;
+    *point_pdf = 1.0;
+    V mw = -(*wi);
+    V wc = mw.x * sc.w2c[0] + mw.y * sc.w2c[1] + mw.z * sc.w2c[2];
+    wc.z = -wc.z;
+    R cos_t = P::cos_acos(wc.z);
+    R denom = 4 * tanh_ * tanv_ / P::pow4(cos_t);
+    *dir_pdf = ((*dist) * (*dist)) / cos_t;
+    *normal = -(*wi);
+    wc /= wc.z;
+    R fx = ((wc.x / tanh_ + 1) * R(0.5)) * W;
+    R fy = ((wc.y / tanv_ + 1) * R(0.5)) * H;
+    // C++ float->int truncation; NaN / out-of-int-range -> -1 (never splatted), see DESIGN.md.
+    *x = (fx > R(-1) && fx < R(W)) ? (int)fx : -1;
+    *y = (fy > R(-1) && fy < R(H)) ? (int)fy : -1;
+    return V(R(1.)) / denom;
+  }
+
+  // ---------------- BDPT (bidirection.cpp) ----------------
+  void prepare_subpath(Ray<R> r, R point_pdf, R dir_pdf, std::vector<Vertex>& path,
+                       const V& init_radiance, const V& init_normal, bool is_light) {  // :20-102
+    Vertex v;
+    path.push_back(v);
+    v.p = point_pdf;
+    v.alpha = init_radiance / point_pdf;
+    v.isect.n = init_normal;
+    v.position = r.o;
+    v.q = 1.;
+    v.is_light = is_light;
+    v.dir_pdf = dir_pdf;
+    path.push_back(v);
+    int i = 2;
+    Isect isect;
+    R prev_pdf = dir_pdf;
+    V prev_f(1., 1., 1.), prev_n(init_normal);
+    while (intersect(r, &isect, true)) {
+      r.max_t = isect.t;  // (not read again: the next ray is rebuilt below)
+      Frame<R> f = make_coord_space(isect.n);
+      const V hit_p = r.o + r.d * isect.t;
+      const V w_out = f.to_local(-r.d);
+      V wi, fv, wi_world;
+      R pdf;
+      fv = bsdf_sample_f(isect.mat, w_out, &wi, &pdf);
+      wi_world = f.to_world(wi);
+      wi_world.normalize();
+      v.isect = isect;
+      R g = std::fabs(dot(prev_n, r.d) * dot(isect.n, r.d)) / (isect.t * isect.t);
+      v.p = path[i - 1].p * prev_pdf * g;
+      v.alpha = path[i - 1].alpha * std::fabs(dot(prev_n, r.d)) * prev_f / prev_pdf;
+      v.position = hit_p;
+      v.is_light = false;
+      Ray<R> ray;
+      ray.o = hit_p; ray.d = wi_world; ray.min_t = R(EPS_F); ray.max_t = (R)INFINITY;
+      r = ray;
+      R p_keep = 1;
+      v.q = p_keep;
+      path.push_back(v);
+      if (i >= max_depth + 1) break;
+      prev_f = fv;
+      prev_n = isect.n;
+      prev_pdf = pdf * p_keep;
+      i++;
+    }
+  }
+  Ray<R> sample_light_ray(R& point_pdf, R& dir_pdf, V& init_radiance, V& init_normal) {  // :105-118
+    int n = (int)sc.lights.size();
+    int id = pol.rand_light(n);
+    Ray<R> r;
+    V rad = light_sample_Le(sc.lights[id], &r, &point_pdf, &dir_pdf, &init_normal);
+    point_pdf /= R(n);
+    init_radiance = rad;
+    r.min_t = R(EPS_F);
+    return r;
+  }
+
+  R mis_weight(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L,
+               const Vertex& LS, const Vertex& ES) {                          // :121-293
+    R w_inv = 0., ratio = 1.;
+    w_inv += ratio;
+    const Light<R>* eye_light = nullptr;
+    for (int i = i_eye; i > 1; i--) {
+      const Vertex& cur = E[i];
+      const Vertex& prv = (i == i_eye) ? (i_light == 1 ? LS : L[i_light]) : E[i + 1];
+      const Vertex& nxt = E[i - 1];
+      R nom, denom, p = 0, g;
+      Frame<R> f = make_coord_space(prv.isect.n);
+      V wo, wi_world = cur.position - prv.position;
+      R dist = wi_world.norm();
+      wi_world.normalize();
+      V wi = f.to_local(wi_world);
+      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      if (i_light == 0 && i == i_eye) {
+        bool hit = false;
+        for (size_t j = 0; j < sc.lights.size(); j++) {
+          if (light_contain_point(sc.lights[j], cur.position)) {
+            hit = true;
+            eye_light = &sc.lights[j];
+            g = 1.;
+            R pp, dp;
+            light_sample_pdf(sc.lights[j], cur.position, V(), &pp, &dp);
+            p = pp;
+            break;
+          }
+        }
+        if (!hit) return 0.;
+      } else if (i_light == 1 && i == i_eye) {
+        p = LS.dir_pdf * LS.q;
+      } else if (i_light == 0 && i == i_eye - 1) {
+        R pp, dp;
+        V w = -wi_world;
+        light_sample_pdf(*eye_light, prv.position, w, &pp, &dp);
+        p = dp * L[1].q;
+      } else {
+        p = bsdf_sample_pdf(prv.isect.mat, wo, wi) * prv.q;
+      }
+      nom = p * g;
+      f = make_coord_space(nxt.isect.n);
+      wi_world = cur.position - nxt.position;
+      dist = wi_world.norm();
+      wi_world.normalize();
+      wi = f.to_local(wi_world);
+      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      if (i == 2) {
+        p = 1.;
+        g = 1.;
+      } else {
+        p = bsdf_sample_pdf(nxt.isect.mat, wo, wi) * nxt.q;
+      }
+      denom = p * g;
+      ratio *= nom / denom;
+      if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
+      w_inv += ratio * ratio;
+    }
+    ratio = 1.;
+    for (int i = i_light; i > 0; i--) {
+      const Vertex& cur = L[i];
+      const Vertex& prv = (i == i_light) ? (i_eye == 1 ? ES : E[i_eye]) : L[i + 1];
+      const Vertex& nxt = L[i - 1];
+      R nom, denom, p, g;
+      Frame<R> f = make_coord_space(prv.isect.n);
+      V wo, wi_world = cur.position - prv.position;
+      R dist = wi_world.norm();
+      wi_world.normalize();
+      V wi = f.to_local(wi_world);
+      if (i_eye <= 1 && i == i_light) p = ES.dir_pdf * ES.q;
+      else p = bsdf_sample_pdf(prv.isect.mat, wo, wi) * prv.q;
+      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      nom = p * g;
+      if (i > 1) {
+        f = make_coord_space(nxt.isect.n);
+        wi_world = cur.position - nxt.position;
+        dist = wi_world.norm();
+        wi_world.normalize();
+        wi = f.to_local(wi_world);
+        if (i == 2) p = nxt.dir_pdf;
+        else p = bsdf_sample_pdf(nxt.isect.mat, wo, wi) * nxt.q;
+        g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+        denom = p * g;
+      } else {
+        denom = cur.p;
+      }
+      ratio *= nom / denom;
+      if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
+      w_inv += ratio * ratio;
+    }
+    return R(1.) / w_inv;
+  }
+
+  void splat(int x, int y, const V& s) {
+    size_t k = 3 * ((size_t)x + (size_t)y * W);
+    for (int c = 0; c < 3; c++) (*light_buf)[k + c] += (double)s[c];
+    if (sample_buf)
+      for (int c = 0; c < 3; c++) (*sample_buf)[k + c] += (double)s[c];
+  }
+
+  V estimate(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L) {  // :296-469
+    Vertex ve, vl, LS, ES;
+    int eye_x = -1, eye_y = -1;
+    ve = E[i_eye];
+    vl = L[i_light];
+    V c;
+    if (i_light == 0) {
+      if (i_eye > 1) {
+        c = get_emission(E[i_eye].isect.mat);
+        if (c.norm() > R(EPS_F)) {
+          bool hit = false;
+          for (size_t j = 0; j < sc.lights.size(); j++) {
+            if (light_contain_point(sc.lights[j], E[i_eye].position)) {
+              hit = true;
+              R pp, dp;
+              V wi = E[i_eye].position - E[i_eye - 1].position;
+              wi.normalize();
+              c = light_sample_pdf(sc.lights[j], E[i_eye].position, wi, &pp, &dp);
+              break;
+            }
+          }
+          if (!hit) c = V();
+        }
+      }
+    } else {
+      V f_eye, f_light, connect;
+      if (i_light == 1) {
+        int n = (int)sc.lights.size();
+        int id = pol.rand_light(n);
+        V ldir, lpoint, ln;
+        R lpp, ldp, dist;
+        V rad = light_sample_Le_point(sc.lights[id], E[i_eye].position, &ldir, &lpoint, &dist, &lpp,
+                                      &ldp, &ln);
+        lpp /= R(n);
+        LS.p = lpp;
+        LS.alpha = rad / lpp;
+        LS.q = 1.;
+        LS.position = lpoint;
+        LS.isect.n = ln;
+        LS.is_light = true;
+        LS.new_sample = true;
+        LS.dir_pdf = ldp;
+        f_light = V(1., 1., 1.);
+        vl = LS;
+      }
+      if (i_eye == 1) {
+        V edir, epoint, en;
+        R epp, edp, dist;
+        V rad = sample_ray_pdf(vl.position, &edir, &epoint, &dist, &epp, &edp, &en, &eye_x, &eye_y);
+        ES.p = epp;
+        ES.alpha = rad / epp;
+        ES.q = 1.;
+        ES.position = epoint;
+        ES.isect.n = en;
+        ES.is_light = false;
+        ES.new_sample = true;
+        ES.dir_pdf = edp;
+        f_eye = V(1., 1., 1.);
+        ve = ES;
+      }
+      if (i_eye > 1) {
+        Frame<R> f = make_coord_space(E[i_eye].isect.n);
+        V er = E[i_eye - 1].position - E[i_eye].position;
+        er.normalize();
+        er = f.to_local(er);
+        connect = vl.position - E[i_eye].position;
+        connect.normalize();
+        connect = f.to_local(connect);
+        f_eye = bsdf_f(E[i_eye].isect.mat, er, connect);
+      }
+      if (i_light > 1) {
+        Frame<R> f = make_coord_space(L[i_light].isect.n);
+        V lr = L[i_light - 1].position - L[i_light].position;
+        lr.normalize();
+        lr = f.to_local(lr);
+        connect = ve.position - L[i_light].position;
+        connect.normalize();
+        connect = f.to_local(connect);
+        f_light = bsdf_f(L[i_light].isect.mat, connect, lr);
+      }
+      connect = vl.position - ve.position;
+      R dist = connect.norm();
+      connect.normalize();
+      Ray<R> r;
+      r.o = ve.position;
+      r.d = connect;
+      r.min_t = R(EPS_F);
+      r.max_t = dist - R(EPS_F);
+      Isect is;
+      if (intersect(r, &is, false)) return V();
+      R g = std::fabs(dot(vl.isect.n, connect) * dot(ve.isect.n, connect)) / (dist * dist);
+      c = f_eye * g * f_light;
+    }
+    V la = i_light == 1 ? LS.alpha : L[i_light].alpha;
+    V ea = i_eye == 1 ? ES.alpha : E[i_eye].alpha;
+    R w = 0.;
+    V contrib = ea * la * c;
+    if (contrib.norm() > R(EPS_F)) w = mis_weight(i_eye, i_light, E, L, LS, ES);
+    V ill = contrib * w;
+    if (i_eye == 1) {
+      if (eye_x >= 0 && eye_y >= 0 && eye_x < W && eye_y < H) splat(eye_x, eye_y, ill / R(ns_aa));
+      return V();
+    }
+    return ill;
+  }
+
+  V est_radiance(const Ray<R>& r) {                                           // :472-500
+    V L_out;
+    std::vector<Vertex> E, L;
+    E.reserve(max_depth + 2);
+    L.reserve(max_depth + 2);
+    prepare_subpath(r, 1., 1., E, V(1., 1., 1.), r.d, false);
+    R lpp, ldp;
+    V lrad, ln;
+    Ray<R> lr = sample_light_ray(lpp, ldp, lrad, ln);
+    prepare_subpath(lr, lpp, ldp, L, lrad, ln, true);
+    for (int i = 1; i < (int)E.size(); i++)
+      for (int j = 0; j < (int)L.size(); j++) L_out += estimate(i, j, E, L);
+    return L_out;
+  }
+
+  // One sample of pixel (x,y) (bidirection.cpp:515-533).
+  V one_sample(int x, int y) {
+    R px, py;
+    grid2d(&px, &py);
+    px = px + R(x);
+    py = py + R(y);
+    R dx = px / R(W), dy = py / R(H);
+    Ray<R> ray = generate_ray(dx, dy);
+    return est_radiance(ray);
+  }
+};
+
+// ----------------------------------------------------------------------------------------------
+template <class R>
+static int render_counter(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, uint64_t seed,
+                          int s0, int sc_count, int nthreads, double* eye, double* light, double* stats) {
+  Scene<R> sc;
+  std::string err;
+  int rc = load_scene<R>(d, sc, err);
+  if (rc) { fprintf(stderr, "oracle: %s\n", err.c_str()); return rc; }
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::vector<double>> lbuf(nthreads, std::vector<double>((size_t)W * H * 3, 0.0));
+  std::vector<Stats> sts(nthreads);
+  auto work = [&](int t) {
+    for (int y = t; y < H; y += nthreads) {
+      for (int x = 0; x < W; x++) {
+        double acc[3] = {0, 0, 0};
+        for (int s = s0; s < s0 + sc_count; s++) {
+          CounterStream cs;
+          cs.init(seed, (uint32_t)(x + y * W), (uint32_t)s);
+          typedef typename std::conditional<sizeof(R) == 8, PolicyC64, PolicyC32>::type P;
+          P pol;
+          pol.cs = &cs;
+          Tracer<P> tr(sc, pol, max_depth, W, H, spp);
+          tr.light_buf = &lbuf[t];
+          V3<R> ill = tr.one_sample(x, y);
+          R inv = R(1.) / R(spp);
+          for (int c = 0; c < 3; c++) acc[c] += (double)(ill[c] * inv);
+          Stats& S = sts[t];
+          S.rays += tr.st.rays; S.closest += tr.st.closest; S.shadow += tr.st.shadow;
+          S.nodes += tr.st.nodes; S.tri += tr.st.tri; S.sph += tr.st.sph; S.hits += tr.st.hits;
+        }
+        size_t k = 3 * ((size_t)x + (size_t)y * W);
+        for (int c = 0; c < 3; c++) eye[k + c] += acc[c];
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int t = 0; t < nthreads; t++)
+    for (size_t k = 0; k < (size_t)W * H * 3; k++) light[k] += lbuf[t][k];
+  if (stats) {
+    Stats S;
+    for (auto& s : sts) {
+      S.rays += s.rays; S.closest += s.closest; S.shadow += s.shadow; S.nodes += s.nodes;
+      S.tri += s.tri; S.sph += s.sph; S.hits += s.hits;
+    }
+    stats[0] = (double)S.rays; stats[1] = (double)S.closest; stats[2] = (double)S.shadow;
+    stats[3] = (double)S.nodes; stats[4] = (double)S.tri; stats[5] = (double)S.sph;
+    stats[6] = (double)S.hits; stats[7] = (double)sc.nodes.size();
+  }
+  return 0;
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+extern "C" {
+
+// mode 0: the reference's own sequence (tiles of 32 in raster order, pixels row-major inside a
+// tile, ns_aa samples per pixel; raytraced_renderer.cpp:297-301,610-615); writes eye, light and the
+// reference-ordered sample buffer (all fp64). modes 1/2: counter RNG, samples [s0, s0+count).
+int oracle_render(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode,
+                  uint64_t seed, int s0, int count, int nthreads, double* eye, double* light,
+                  double* sample, double* stats) {
+  if (!d || W <= 0 || H <= 0 || spp <= 0 || max_depth < 0) return BDPT_E_INVALID;
+  if (mode == 1) return render_counter<double>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats);
+  if (mode == 2) return render_counter<float>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats);
+  if (mode != 0) return BDPT_E_INVALID;
+  Scene<double> sc;
+  std::string err;
+  int rc = load_scene<double>(d, sc, err);
+  if (rc) { fprintf(stderr, "oracle: %s\n", err.c_str()); return rc; }
+  RefStreams rs;                 // fresh engines: the reference's static engines at process start
+  std::srand(1);
+  PolicyRef pol;
+  pol.rs = &rs;
+  Tracer<PolicyRef> tr(sc, pol, max_depth, W, H, spp);
+  std::vector<double> lb((size_t)W * H * 3, 0.0), sb((size_t)W * H * 3, 0.0);
+  tr.light_buf = &lb;
+  tr.sample_buf = &sb;
+  const int TS = 32;
+  for (int ty = 0; ty < H; ty += TS)
+    for (int tx = 0; tx < W; tx += TS)
+      for (int y = ty; y < std::min(ty + TS, H); y++)
+        for (int x = tx; x < std::min(tx + TS, W); x++) {
+          V3<double> illum(0, 0, 0);                                           // :514-541
+          for (int s = 0; s < spp; s++) illum += tr.one_sample(x, y);
+          illum /= (double)spp;
+          size_t k = 3 * ((size_t)x + (size_t)y * W);
+          for (int c = 0; c < 3; c++) { eye[k + c] = illum[c]; sb[k + c] += illum[c]; }
+        }
+  memcpy(light, lb.data(), lb.size() * sizeof(double));
+  if (sample) memcpy(sample, sb.data(), sb.size() * sizeof(double));
+  if (stats) {
+    stats[0] = (double)tr.st.rays; stats[1] = (double)tr.st.closest; stats[2] = (double)tr.st.shadow;
+    stats[3] = (double)tr.st.nodes; stats[4] = (double)tr.st.tri; stats[5] = (double)tr.st.sph;
+    stats[6] = (double)tr.st.hits; stats[7] = (double)sc.nodes.size();
+  }
+  return 0;
+}
+
+// BVH facts of the oracle's reference build: nodes, depth, DFS leaf order (prim indices).
+int oracle_bvh_info(const bdpt_scene_desc* d, int* nodes, int* depth, int* leaf_order) {
+  Scene<double> sc;
+  std::string err;
+  int rc = load_scene<double>(d, sc, err);
+  if (rc) return rc;
+  *nodes = (int)sc.nodes.size();
+  *depth = sc.depth;
+  if (leaf_order)
+    for (size_t i = 0; i < sc.leaf_prims.size(); i++) leaf_order[i] = sc.leaf_prims[i];
+  return 0;
+}
+
+// Closest-hit / any-hit queries (mode 1: fp64 boxes; mode 2: fp32 conservative boxes).
+int oracle_trace_rays(const bdpt_scene_desc* d, int mode, const float* rays, int n, int any_hit,
+                      float* out_t, int* out_prim) {
+  if (mode == 2) {
+    Scene<float> sc;
+    std::string err;
+    if (load_scene<float>(d, sc, err)) return BDPT_E_INVALID;
+    CounterStream cs;
+    cs.init(0, 0, 0);
+    PolicyC32 pol;
+    pol.cs = &cs;
+    Tracer<PolicyC32> tr(sc, pol, 1, 1, 1, 1);
+    for (int i = 0; i < n; i++) {
+      const float* r = rays + 8 * (size_t)i;
+      Ray<float> ray;
+      ray.o = V3<float>(r[0], r[1], r[2]);
+      ray.d = V3<float>(r[3], r[4], r[5]);
+      ray.min_t = r[6];
+      ray.max_t = r[7];
+      Tracer<PolicyC32>::Isect is;
+      bool h = tr.intersect(ray, &is, !any_hit);
+      out_t[i] = h ? (any_hit ? 0.0f : is.t) : INFINITY;
+      out_prim[i] = h ? (any_hit ? 0 : is.prim) : -1;
+    }
+    return 0;
+  }
+  Scene<double> sc;
+  std::string err;
+  if (load_scene<double>(d, sc, err)) return BDPT_E_INVALID;
+  CounterStream cs;
+  cs.init(0, 0, 0);
+  PolicyC64 pol;
+  pol.cs = &cs;
+  Tracer<PolicyC64> tr(sc, pol, 1, 1, 1, 1);
+  for (int i = 0; i < n; i++) {
+    const float* r = rays + 8 * (size_t)i;
+    Ray<double> ray;
+    ray.o = V3<double>(r[0], r[1], r[2]);
+    ray.d = V3<double>(r[3], r[4], r[5]);
+    ray.min_t = r[6];
+    ray.max_t = r[7];
+    Tracer<PolicyC64>::Isect is;
+    bool h = tr.intersect(ray, &is, !any_hit);
+    out_t[i] = h ? (any_hit ? 0.0f : (float)is.t) : INFINITY;
+    out_prim[i] = h ? (any_hit ? 0 : is.prim) : -1;
+  }
+  return 0;
+}
+
+// Known-answer helpers for the RNG and the deterministic transcendentals.
+void oracle_philox(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t block, uint32_t out[4]) {
+  out[0] = pixel; out[1] = sample; out[2] = block; out[3] = 0xB1D1u;
+  philox4x32_10(out, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+void oracle_cos_sin_2pi(float u, float* c, float* s) { cos_sin_2pi_f32(u, c, s); }
+double oracle_mt_first(int n, double* out) {   // first n U of a fresh reference engine
+  RefStreams rs;
+  for (int i = 0; i < n; i++) out[i] = rs.uS();
+  return n > 0 ? out[0] : 0.0;
+}
+
+}  // extern "C"
