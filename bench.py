@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark of the BDPT hot path on MI355X (BASELINE.json metric: Msamples/s at m=5, plus
+per-pixel RMSE vs the CPU path at a matched seed).
+
+Workload (N=1): BASELINE.json configs[1] — dae/sky/CBspheres.dae (mirror + glass spheres),
+480x360, 128 spp, -m 5, on one MI355X. One "step" = one full-frame render of 128 samples per
+pixel (22.1 M pixel-samples) through the C-ABI (libbdpt_amd.so, k_bdpt_sample).
+Multi-GPU (torchrun, one rank per GPU): weak scaling — rank r renders the global sample range
+[r*128, (r+1)*128) of every pixel (sample keys are global, so the image is independent of the
+rank count up to fp32 summation order) and the W*H*3 fp32 frames are summed over RCCL (xGMI)
+onto rank 0 inside the timed region. value = all ranks' samples / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "bidirectional-pathtracing_amd")
+for p in (PKG, os.path.join(REPO, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "Msamples/sec (spp×pixels/s) at m=5; per-pixel RMSE vs CPU at matched seed"
+SCENE, W, H, SPP, M = "CBspheres", 480, 360, 128, 5
+HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BYTES_NODE, BYTES_TRI, BYTES_SPH, BYTES_HIT = 32, 36, 16, 40
+
+
+def algorithmic_bytes(st) -> int:
+    return (BYTES_NODE * st.node_visits + BYTES_TRI * st.tri_tests + BYTES_SPH * st.sph_tests
+            + BYTES_HIT * st.hits)
+
+
+def cpu_baseline(scene, threads: int, budget_s: float = 12.0) -> dict:
+    """The oracle's fp64 reference-semantics path (mode COUNTER64: the reference's arithmetic,
+    multi-threaded like the reference's -t N) timed on this host on a bounded sample of the same
+    workload (full 480x360 frame, a few spp)."""
+    from _util import MODE_C64, oracle_render
+    done, t_tot, spp_run = 0, 0.0, 1
+    s0 = 0
+    while t_tot < budget_s and spp_run <= 64:
+        t0 = time.perf_counter()
+        oracle_render(scene, W, H, SPP, M, MODE_C64, seed=5489, s0=s0, count=spp_run, threads=threads)
+        dt = time.perf_counter() - t0
+        t_tot += dt
+        done += W * H * spp_run
+        s0 += spp_run
+        rate = W * H * spp_run / dt
+        spp_run = max(1, int((budget_s - t_tot) * rate / (W * H)))
+        if t_tot >= budget_s * 0.6:
+            break
+    return {"value": done / t_tot / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{SCENE} {W}x{H}, {done // (W * H)} spp of 128, m={M}, oracle fp64 "
+                      f"(reference arithmetic) with {threads} threads, {t_tot:.1f} s"}
+
+
+def parity_check(scene, seed: int) -> dict:
+    """Per-pixel RMSE of the GPU sample buffer vs the oracle's COUNTER32 CPU path, same seed,
+    same workload at 2 spp (the CPU side of the metric)."""
+    import numpy as np
+    import bdpt_amd as B
+    from _util import MODE_C32, oracle_render
+    S = 2
+    pt = B.BidirectionalPathTracer(scene, W, H, S, M, seed=seed)
+    pt.raytrace_tiles()
+    g = pt.read_frame(B.FRAME_SAMPLE).astype(np.float64)
+    pt.close()
+    ref = oracle_render(scene, W, H, S, M, MODE_C32, seed=seed,
+                        threads=min(16, os.cpu_count() or 1))[0]
+    return {"rmse": float(np.sqrt(np.mean((g - ref) ** 2))), "spp": S, "tolerance": 1e-4,
+            "cpu": "oracle COUNTER32 (fp32 device semantics)"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--scene", default=SCENE)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import bdpt_amd as B
+    from _util import golden_scene
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    scene = golden_scene(args.scene, W, H)
+    seed = 5489
+    stream = torch.cuda.current_stream(dev)
+    # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
+    pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index)
+    pt.set_stream(stream.cuda_stream)
+    frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+
+    def step(k: int):
+        base = (k * world + rank) * SPP        # fresh global sample range every step
+        pt.raytrace_tiles([], base, SPP)
+        pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
+        if dist is not None:
+            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        base = ((args.warmup + k) * world + rank) * SPP
+        ev[k][0].record(stream)
+        pt.raytrace_tiles([], base, SPP)            # k_bdpt_sample: the dominant kernel
+        ev[k][1].record(stream)
+        pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
+        if dist is not None:
+            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pt.close()
+
+    # algorithmic bytes of one launch: in-kernel counters on a separate, untimed launch of the
+    # same workload (counting perturbs timing), SURVEY.md §8d.
+    ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
+                                   collect_stats=True)
+    ps.raytrace_tiles([], rank * SPP, SPP)
+    st = ps.stats()
+    ps.close()
+    bytes_launch = algorithmic_bytes(st)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+
+    samples_total = W * H * SPP * world * args.steps
+    value = samples_total / elapsed / 1e6
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return 0
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: fixed-seed renders (Philox counter RNG) of the reference's scene "
+                "CBspheres.dae as the reference loads it (tests/golden/scenes)",
+        "config": {"workload": f"{args.scene} {W}x{H} -s {SPP} -m {M} (BASELINE configs[1]) "
+                               f"per GPU, sample-range shards + RCCL sum-reduce",
+                   "scene": args.scene, "width": W, "height": H, "spp_per_gpu": SPP,
+                   "max_depth": M, "parallelism": f"samples x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                     "traffic": traffic, "kernel": "k_bdpt_sample", "kernel_ms": round(kern_ms, 3),
+                     "algorithmic_bytes_per_launch": bytes_launch,
+                     "counts_per_launch": {"node_aabbs": st.node_visits, "tri_tests": st.tri_tests,
+                                           "sph_tests": st.sph_tests, "hits": st.hits,
+                                           "closest_rays": st.closest_rays,
+                                           "shadow_rays": st.shadow_rays}},
+    }
+    if world == 1 and not args.no_parity:
+        out["parity"] = parity_check(scene, seed)
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene, threads=min(16, os.cpu_count() or 1))
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

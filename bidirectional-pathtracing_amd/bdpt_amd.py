@@ -219,6 +219,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_sync.argtypes = [C.c_void_p]
     lib.bdpt_read_frame.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_float)]
     lib.bdpt_frame_device_ptr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bdpt_copy_frame.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.bdpt_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
     lib.bdpt_trace_rays.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_int32,
                                     C.POINTER(C.c_float), C.POINTER(C.c_int32)]
@@ -301,6 +302,9 @@ class BidirectionalPathTracer:
         p = C.c_void_p()
         _check(self.lib.bdpt_frame_device_ptr(self.ctx, which, C.byref(p)), self.lib)
         return int(p.value or 0)
+
+    def copy_frame(self, which: int, dst_device_ptr: int) -> None:
+        _check(self.lib.bdpt_copy_frame(self.ctx, which, C.c_void_p(dst_device_ptr)), self.lib)
 
     def stats(self) -> Stats:
         s = Stats()

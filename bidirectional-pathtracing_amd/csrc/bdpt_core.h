@@ -1,0 +1,987 @@
+// bdpt_core.h — device-side BDPT per-sample pipeline for MI355X (gfx950), single-source so the
+// host part of libbdpt_amd.so can precompute light frames with the same arithmetic.
+//
+// What it computes is the reference's per-pixel-sample estimator
+//   BidirectionalPathTracer::raytrace_pixel / est_radiance_global_illumination
+//   (src/pathtracer/bidirection.cpp:472-542)
+// in the fp32 "device semantics" of DESIGN.md §fp32: every expression keeps the reference's
+// operation order (CGL Vector3D semantics), uniforms come from Philox4x32-10 keyed by
+// (seed, pixel, sample), sin/cos(2*pi*u) from a fixed polynomial, cos(acos z) = z, integer
+// powers by products, and the sphere quadratic in fp64. The oracle's COUNTER32 mode
+// (oracle/bdpt_oracle.cpp) restates the same semantics independently; parity is per sample.
+//
+// How it differs from the reference's *structure* (output-identical):
+//  * BVH2 with both child boxes in the parent, near-first ordered traversal, t-culling against
+//    conservatively padded fp32 boxes; ties in t resolved to the larger DFS leaf position, which
+//    is what the reference's l->r exhaustive traversal with `t <= max_t` yields (bvh.cpp:161-188).
+//  * Connection (shadow) rays use an any-hit traversal: only their boolean is consumed
+//    (bidirection.cpp:428-433).
+//  * The MIS walk (bidirection.cpp:121-293) is O(i+j) multiplies per connection: the per-vertex
+//    ratios nom/denom of the non-endpoint steps are path constants, evaluated once per subpath
+//    with the reference's exact operations and reused; only the two endpoint steps are evaluated
+//    per connection.
+//  * Connections whose contribution is identically zero (non-diffuse endpoint BSDF, f = 0
+//    hemisphere test, zero throughput) skip their shadow ray (quirk 17).
+
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BDPT_HD __host__ __device__ __forceinline__
+#define BDPT_D __device__ __forceinline__
+#else
+#include <cmath>
+#define BDPT_HD inline
+#define BDPT_D inline
+#include <cstring>
+using std::sqrt;
+struct float4 {
+  float x, y, z, w;
+};
+inline int __float_as_int(float f) { int i; std::memcpy(&i, &f, 4); return i; }
+#endif
+
+namespace bdpt {
+
+// ------------------------------------------------------------------------------------------------
+// Constants (CGL/include/CGL/misc.h:11-14)
+#define BDPT_PI_F 3.14159265358979323f
+#define BDPT_EPS_F 0.00001f
+
+// ------------------------------------------------------------------------------------------------
+// fp32 3-vectors with CGL Vector3D operation order (vector3D.h)
+struct f3 {
+  float x, y, z;
+};
+BDPT_HD f3 mk3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+BDPT_HD f3 add(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+BDPT_HD f3 sub(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+BDPT_HD f3 mul(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+BDPT_HD f3 muls(f3 a, float c) { return mk3(a.x * c, a.y * c, a.z * c); }      // v * c
+BDPT_HD f3 smul(float c, f3 a) { return mk3(c * a.x, c * a.y, c * a.z); }      // c * v
+BDPT_HD f3 divs(f3 a, float c) { float rc = 1.0f / c; return mk3(rc * a.x, rc * a.y, rc * a.z); }
+BDPT_HD f3 neg(f3 a) { return mk3(-a.x, -a.y, -a.z); }
+BDPT_HD float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+BDPT_HD float norm2(f3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+BDPT_HD float norm(f3 a) { return sqrtf(norm2(a)); }
+BDPT_HD f3 normalize(f3 a) { float rc = 1.0f / norm(a); return mk3(a.x * rc, a.y * rc, a.z * rc); }
+BDPT_HD f3 cross(f3 u, f3 v) {
+  return mk3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+BDPT_HD f3 splat3(float c) { return mk3(c, c, c); }
+
+// make_coord_space (bsdf.cpp:21-41): columns X, Y, Z of o2w.
+struct Frame {
+  f3 X, Y, Z;
+};
+BDPT_HD Frame make_frame(f3 n) {
+  f3 z = n, h = n;
+  if (fabsf(h.x) <= fabsf(h.y) && fabsf(h.x) <= fabsf(h.z)) h.x = 1.0f;
+  else if (fabsf(h.y) <= fabsf(h.x) && fabsf(h.y) <= fabsf(h.z)) h.y = 1.0f;
+  else h.z = 1.0f;
+  z = normalize(z);
+  f3 y = normalize(cross(h, z));
+  f3 x = normalize(cross(z, y));
+  Frame f;
+  f.X = x; f.Y = y; f.Z = z;
+  return f;
+}
+// o2w * v (matrix3x3.cpp:110-114) and w2o * v = o2w.T() * v
+BDPT_HD f3 to_world(const Frame& f, f3 v) { return add(add(smul(v.x, f.X), smul(v.y, f.Y)), smul(v.z, f.Z)); }
+BDPT_HD float lz(f3 v, f3 Z) { return v.x * Z.x + v.y * Z.y + v.z * Z.z; }   // (w2o*v).z
+BDPT_HD f3 to_local(const Frame& f, f3 v) { return mk3(lz(v, f.X), lz(v, f.Y), lz(v, f.Z)); }
+BDPT_HD f3 zaxis(f3 n) { return normalize(n); }   // make_coord_space(n).Z without X, Y
+
+// ------------------------------------------------------------------------------------------------
+// Counter RNG: Philox4x32-10, counter (pixel, sample, block, 0xB1D1), key (seed lo, hi).
+struct Rng {
+  uint32_t k0, k1, pix, smp, block;
+  uint32_t b0, b1, b2, b3;
+  int idx;
+};
+BDPT_HD void rng_init(Rng& r, uint64_t seed, uint32_t pixel, uint32_t sample) {
+  r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32); r.pix = pixel; r.smp = sample;
+  r.block = 0; r.idx = 4;
+}
+BDPT_HD void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+BDPT_HD float u_of(uint32_t x) { return ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-07f; }
+BDPT_HD float rng_next(Rng& r) {
+  if (r.idx == 4) {
+    r.b0 = r.pix; r.b1 = r.smp; r.b2 = r.block++; r.b3 = 0xB1D1u;
+    philox(r.b0, r.b1, r.b2, r.b3, r.k0, r.k1);
+    r.idx = 0;
+  }
+  uint32_t x = r.idx == 0 ? r.b0 : r.idx == 1 ? r.b1 : r.idx == 2 ? r.b2 : r.b3;
+  r.idx++;
+  return u_of(x);
+}
+
+// cos/sin(2*pi*u), u in (0,1): quadrant split + Taylor polynomials (same as the oracle's).
+BDPT_HD void cos_sin_2pi(float u, float* c, float* s) {
+  float t = u * 4.0f;
+  int k = (int)(t + 0.5f);
+  float f = u - (float)k * 0.25f;
+  float f2 = f * f;
+  float sp = f * (6.2831854820251465f +
+                  f2 * (-41.34170150756836f +
+                        f2 * (81.6052474975586f + f2 * (-76.70585632324219f + f2 * 42.058692932128906f))));
+  float cp = 1.0f + f2 * (-19.739208221435547f +
+                          f2 * (64.93939208984375f +
+                                f2 * (-85.45681762695312f + f2 * (60.2446403503418f + f2 * -26.42625617980957f))));
+  int q = k & 3;
+  float cc = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
+  float ss = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
+  *c = cc;
+  *s = ss;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Scene layout in HBM (see DESIGN.md §Data layout)
+enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REFRACTION = 4 };
+enum { LIGHT_AREA = 0, LIGHT_POINT = 1 };
+
+struct DMat {
+  int type;
+  float a[3];
+  float b[3];
+  float ior;
+};
+struct DLight {
+  int type;
+  float rad[3], pos[3], dir[3], dx[3], dy[3];
+  float area;
+  float fx[3], fy[3], fz[3];  // make_coord_space(dir)
+};
+struct DCam {
+  float pos[3];
+  float c2w[9];  // column-major
+  float w2c[9];
+  float tanh_, tanv_;  // tan(hFov*PI/360) in fp64, rounded (camera.cpp:199-200)
+  float nclip, fclip;
+};
+
+// Child reference: >= 0 internal node index; < 0 leaf: ~ref = start << 7 | sphere_mask << 3 | count.
+BDPT_HD bool ref_is_leaf(int r) { return r < 0; }
+BDPT_HD int leaf_start(int r) { return (int)(((uint32_t)~r) >> 7); }
+BDPT_HD int leaf_count(int r) { return (int)((uint32_t)~r & 7u); }
+BDPT_HD int leaf_sph_mask(int r) { return (int)((((uint32_t)~r) >> 3) & 15u); }
+
+struct SceneView {
+  const float4* nodes;   // 4 x float4 per node: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
+  const float4* geom;    // 3 x float4 per prim (DFS order): tri p0,e1,e2 | sphere c,r
+  const float4* shade;   // 3 x float4 per prim: n1 n2 n3 (tri) ; w of the 3rd = material (bits)
+  const DMat* mats;
+  const DLight* lights;
+  int nlights;
+  int root;              // root child reference
+  DCam cam;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Counters for the roofline (algorithmic bytes)
+struct Counters {
+  uint32_t nodes, tris, sphs, closest, shadow, hits;
+};
+
+struct Hit {
+  float t;
+  int prim;   // DFS position, -1 = none
+  float b1, b2;
+};
+
+// Möller–Trumbore exactly as Triangle::intersect (triangle.cpp:57-95), fp32.
+BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f3 d, float tmin, float tmax,
+                      float* t_out, float* b1_out, float* b2_out) {
+  f3 p0 = mk3(g0.x, g0.y, g0.z);
+  f3 e1 = mk3(g0.w, g1.x, g1.y);
+  f3 e2 = mk3(g1.z, g1.w, g2.x);
+  f3 s = sub(o, p0);
+  f3 s1 = cross(d, e2), s2 = cross(s, e1);
+  float denom = dot(s1, e1);
+  float t = dot(s2, e2) / denom;
+  float b1 = dot(s1, s) / denom;
+  float b2 = dot(s2, d) / denom;
+  *t_out = t; *b1_out = b1; *b2_out = b2;
+  return t >= tmin && t <= tmax && b1 >= 0 && b2 >= 0 && b1 + b2 <= 1;
+}
+
+// Sphere::test + intersect (sphere.cpp:11-35,61-93) with the quadratic in fp64.
+BDPT_HD bool sph_test(const float4 g0, f3 o, f3 d, float tmin, float tmax, float* t_out) {
+  double ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
+  double cx = g0.x, cy = g0.y, cz = g0.z, r = g0.w;
+  double r2 = r * r;
+  double a = dx * dx + dy * dy + dz * dz;
+  double fx = ox - cx, fy = oy - cy, fz = oz - cz;
+  double b = 2 * (fx * dx + fy * dy + fz * dz);
+  double c = (fx * fx + fy * fy + fz * fz) - r2;
+  double delta = b * b - 4 * a * c;
+  if (delta < 0) return false;
+  double root = sqrt(delta);
+  double t1 = (-b - root) / (2 * a);
+  double t2 = (-b + root) / (2 * a);
+  double t = -1;
+  if (t1 >= (double)tmin && t1 <= (double)tmax) t = t1;
+  else if (t2 >= (double)tmin && t2 <= (double)tmax) t = t2;
+  if (t > 0) {
+    *t_out = (float)t;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace bdpt
+
+namespace bdpt {
+
+// ------------------------------------------------------------------------------------------------
+// BVH traversal (replaces BVHAccel::intersect, bvh.cpp:161-188; see header comment).
+#ifndef BDPT_STACK
+#define BDPT_STACK 64
+#endif
+
+struct RayInv {
+  f3 o, d, inv;
+};
+BDPT_HD RayInv make_rayinv(f3 o, f3 d) {
+  RayInv r;
+  r.o = o; r.d = d;
+  r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  return r;
+}
+// Slab test against a padded (conservative) box. NaN lanes (0 * inf) are ignored by fmin/fmax.
+BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, float hy, float hz,
+                  float* tn, float* tf) {
+  float t0x = (lx - r.o.x) * r.inv.x, t1x = (hx - r.o.x) * r.inv.x;
+  float t0y = (ly - r.o.y) * r.inv.y, t1y = (hy - r.o.y) * r.inv.y;
+  float t0z = (lz_ - r.o.z) * r.inv.z, t1z = (hz - r.o.z) * r.inv.z;
+  float n = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+  float f = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+  *tn = n;
+  *tf = f * 1.00000024f;
+}
+
+// Closest hit in [tmin, tmax]; ties in t go to the larger DFS position (reference order).
+BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Hit& h, Counters& c) {
+  RayInv r = make_rayinv(o, d);
+  h.t = tmax;
+  h.prim = -1;
+  h.b1 = 0; h.b2 = 0;
+  int stack[BDPT_STACK];
+  int sp = 0;
+  int ref = S.root;
+  c.closest++;
+  for (;;) {
+    if (ref_is_leaf(ref)) {
+      int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+      for (int k = 0; k < cnt; k++) {
+        int pi = st + k;
+        float t, b1 = 0, b2 = 0;
+        bool ok;
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(S.geom[3 * pi], o, d, tmin, h.t, &t);
+        } else {
+          c.tris++;
+          ok = tri_test(S.geom[3 * pi], S.geom[3 * pi + 1], S.geom[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
+        }
+        if (ok && (t < h.t || pi > h.prim)) {   // t <= h.t here: t == h.t only replaces a lower DFS index
+          h.t = t; h.prim = pi; h.b1 = b1; h.b2 = b2;
+        }
+      }
+      if (sp == 0) break;
+      ref = stack[--sp];
+      continue;
+    }
+    const float4* N = S.nodes + 4 * ref;
+    float4 a = N[0], b = N[1], cc = N[2], e = N[3];
+    c.nodes += 2;
+    float tnl, tfl, tnr, tfr;
+    slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
+    slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
+    bool hl = tnl <= tfl && tnl <= h.t && tfl >= tmin;
+    bool hr = tnr <= tfr && tnr <= h.t && tfr >= tmin;
+    int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
+    if (hl && hr) {
+      int nearr = tnl <= tnr ? lref : rref;
+      int farr = tnl <= tnr ? rref : lref;
+      stack[sp++] = farr;
+      ref = nearr;
+    } else if (hl) {
+      ref = lref;
+    } else if (hr) {
+      ref = rref;
+    } else {
+      if (sp == 0) break;
+      ref = stack[--sp];
+    }
+  }
+  if (h.prim >= 0) c.hits++;
+  return h.prim >= 0;
+}
+
+// Any hit in [tmin, tmax] (connection rays, bidirection.cpp:418-433).
+BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
+  RayInv r = make_rayinv(o, d);
+  int stack[BDPT_STACK];
+  int sp = 0;
+  int ref = S.root;
+  c.shadow++;
+  for (;;) {
+    if (ref_is_leaf(ref)) {
+      int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+      for (int k = 0; k < cnt; k++) {
+        int pi = st + k;
+        float t, b1, b2;
+        bool ok;
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(S.geom[3 * pi], o, d, tmin, tmax, &t);
+        } else {
+          c.tris++;
+          ok = tri_test(S.geom[3 * pi], S.geom[3 * pi + 1], S.geom[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+        }
+        if (ok) return true;
+      }
+      if (sp == 0) return false;
+      ref = stack[--sp];
+      continue;
+    }
+    const float4* N = S.nodes + 4 * ref;
+    float4 a = N[0], b = N[1], cc = N[2], e = N[3];
+    c.nodes += 2;
+    float tnl, tfl, tnr, tfr;
+    slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
+    slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
+    bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
+    bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
+    int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
+    if (hl && hr) {
+      int nearr = tnl <= tnr ? lref : rref;
+      int farr = tnl <= tnr ? rref : lref;
+      stack[sp++] = farr;
+      ref = nearr;
+    } else if (hl) {
+      ref = lref;
+    } else if (hr) {
+      ref = rref;
+    } else {
+      if (sp == 0) return false;
+      ref = stack[--sp];
+    }
+  }
+}
+
+// Shading record of a closest hit: interpolated normal (triangle.cpp:80-82) or sphere normal
+// (sphere.cpp:78-81), and the material.
+BDPT_HD void shade_hit(const SceneView& S, const Hit& h, f3 o, f3 d, f3* n_out, int* mat_out) {
+  const float4* sh = S.shade + 3 * h.prim;
+  float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
+  *mat_out = __float_as_int(s2.y);
+  if (__float_as_int(s2.z) != 0) {   // sphere: center in geom
+    float4 g = S.geom[3 * h.prim];
+    f3 p = add(o, smul(h.t, d));
+    *n_out = normalize(sub(p, mk3(g.x, g.y, g.z)));
+  } else {
+    f3 n1 = mk3(s0.x, s0.y, s0.z), n2 = mk3(s0.w, s1.x, s1.y), n3 = mk3(s1.z, s1.w, s2.x);
+    f3 n = add(add(muls(n1, 1 - h.b1 - h.b2), smul(h.b1, n2)), smul(h.b2, n3));
+    *n_out = normalize(n);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Samplers (sampler.cpp) and BSDFs (bsdf.cpp, advanced_bsdf.cpp)
+BDPT_HD void grid2d(Rng& g, float* x, float* y) {   // Vector2D(U(), U()): y is drawn first
+  float b = rng_next(g);
+  float a = rng_next(g);
+  *x = a;
+  *y = b;
+}
+BDPT_HD f3 cosine_hemi(Rng& g, float* pdf) {   // sampler.cpp:76-86
+  float Xi1 = rng_next(g);
+  float Xi2 = rng_next(g);
+  float r = sqrtf(Xi1);
+  *pdf = sqrtf(1 - Xi1) / BDPT_PI_F;
+  float c, s;
+  cos_sin_2pi(Xi2, &c, &s);
+  return mk3(r * c, r * s, sqrtf(1 - Xi1));
+}
+BDPT_HD float cosine_pdf_z(float z) { return z > 0 ? z / BDPT_PI_F : 0.0f; }   // sampler.cpp:92-95
+
+BDPT_HD bool is_delta(int type) { return type == MAT_MIRROR || type == MAT_GLASS || type == MAT_REFRACTION; }
+
+BDPT_HD bool refract_dir(f3 wo, f3* wi, float ior) {   // advanced_bsdf.cpp:279-303
+  bool enter = wo.z > 0;
+  float eta = enter ? 1.0f / ior : ior;
+  float z_sq = 1 - eta * eta * (1 - wo.z * wo.z);
+  if (z_sq < 0) return false;
+  float sgn = enter ? -1.0f : 1.0f;
+  *wi = mk3(-eta * wo.x, -eta * wo.y, sgn * sqrtf(z_sq));
+  return true;
+}
+
+BDPT_HD f3 sample_f(const DMat& M, Rng& g, f3 wo, f3* wi, float* pdf) {
+  f3 A = mk3(M.a[0], M.a[1], M.a[2]);
+  switch (M.type) {
+    case MAT_DIFFUSE: {
+      *wi = cosine_hemi(g, pdf);
+      if (wo.z < 0 || wi->z < 0) return splat3(0);
+      return divs(A, BDPT_PI_F);
+    }
+    case MAT_EMISSION: {
+      *pdf = 1.0f / BDPT_PI_F;
+      *wi = cosine_hemi(g, pdf);
+      return splat3(0);
+    }
+    case MAT_MIRROR: {
+      *wi = mk3(-wo.x, -wo.y, wo.z);
+      *pdf = 1;
+      float ct = fabsf(wi->z) / norm(*wi);
+      return divs(A, ct);
+    }
+    case MAT_REFRACTION: {
+      f3 B = mk3(M.b[0], M.b[1], M.b[2]);
+      if (!refract_dir(wo, wi, M.ior)) { *pdf = 1; return splat3(0); }
+      *pdf = 1;
+      float eta = wo.z > 0 ? 1.0f / M.ior : M.ior;
+      float ct = fabsf(wi->z) / norm(*wi);
+      return divs(divs(B, ct), eta * eta);
+    }
+    default: {   // glass (advanced_bsdf.cpp:198-237)
+      f3 B = mk3(M.b[0], M.b[1], M.b[2]);
+      f3 wr = mk3(-wo.x, -wo.y, wo.z), wt;
+      bool tir = !refract_dir(wo, &wt, M.ior);
+      if (tir) {
+        *pdf = 1;
+        *wi = wr;
+        float ct = fabsf(wi->z) / norm(wo);
+        return divs(A, ct);
+      }
+      float cref = fabsf(wt.z) / norm(wt);
+      float eta = wo.z > 0 ? 1.0f / M.ior : M.ior;
+      float x = (1 - eta) / (1 + eta);
+      float R0 = x * x;
+      float m = 1 - cref, m2 = m * m, m4 = m2 * m2;
+      float Rf = R0 + (1 - R0) * (m4 * m);
+      if (rng_next(g) < Rf) {
+        *wi = wr;
+        *pdf = Rf;
+        float ct = fabsf(wi->z) / norm(*wi);
+        return divs(smul(Rf, A), ct);
+      }
+      *wi = wt;
+      *pdf = 1 - Rf;
+      float ct = fabsf(wi->z) / norm(*wi);
+      return divs(divs(smul(1 - Rf, B), ct), eta * eta);
+    }
+  }
+}
+
+// BSDF::sample_pdf with wo = 0 (as every MIS call site passes, bidirection.cpp:150,189,...).
+// `n` is the vertex normal (the frame is rebuilt only for glass, which needs wi.x, wi.y).
+BDPT_HD float pdf_b(const DMat& M, f3 n, f3 zh, f3 dw) {
+  switch (M.type) {
+    case MAT_DIFFUSE:
+    case MAT_EMISSION: return cosine_pdf_z(lz(dw, zh));
+    case MAT_MIRROR:
+    case MAT_REFRACTION: return 1.0f;
+    default: {
+      Frame f = make_frame(n);
+      f3 wi = to_local(f, dw), wt;
+      if (!refract_dir(wi, &wt, M.ior)) return 1.0f;
+      float c = fabsf(wt.z) / norm(wt);
+      float eta = M.ior;   // wo = 0: wo.z > 0 is false (advanced_bsdf.cpp:251)
+      float x = (1 - eta) / (1 + eta);
+      float R0 = x * x;
+      float m = 1 - c, m2 = m * m, m4 = m2 * m2;
+      float Rf = R0 + (1 - R0) * (m4 * m);
+      if (wi.z > 0) return Rf;
+      return 1 - Rf;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
+struct Vtx {
+  f3 pos, n, zh, alpha;
+  float woz;   // eye: (w2o*normalize(E[k-1]-E[k])).z ; light: same with L[k-1]  (f() hemisphere test)
+  float fwd;   // MIS denominator of the step at this vertex (bidirection.cpp:194-211 / 257-280)
+  float q;     // rev/fwd ratio of the non-endpoint step (nom/denom with prv = next vertex outward)
+  float revg;  // g of that reverse step (needed by the s=0 special case, :181-187)
+  int mat;     // -1: no BSDF (camera / light vertex)
+};
+
+struct LightSample {
+  f3 pos, n, zh, alpha;
+  float dir_pdf;
+};
+
+template <int MAXV>
+struct Paths {
+  Vtx E[MAXV];       // E[k] at index k-2 (k >= 2): eye hits
+  Vtx L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
+  int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
+  float l1_dir_pdf;
+};
+
+struct SampleParams {
+  int W, H, spp, max_depth;
+  uint64_t seed;
+};
+
+// Subpath random walk (prepare_bidirectional_subpath, bidirection.cpp:20-102).
+template <int MAXV>
+BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, float tmin, float tmax,
+                        float point_pdf, float dir_pdf, f3 init_rad, f3 init_n, int max_depth, Vtx* out) {
+  f3 prev_alpha = divs(init_rad, point_pdf);
+  float prev_pdf = dir_pdf;
+  f3 prev_f = splat3(1.0f), prev_n = init_n;
+  int i = 2, count = 0;
+  f3 ro = o, rd = d;
+  float rmin = tmin, rmax = tmax;
+  for (;;) {
+    Hit h;
+    if (!trace_closest(S, ro, rd, rmin, rmax, h, cnt)) break;
+    f3 n;
+    int mat;
+    shade_hit(S, h, ro, rd, &n, &mat);
+    const DMat M = S.mats[mat];
+    Frame fr = make_frame(n);
+    f3 hit_p = add(ro, muls(rd, h.t));
+    f3 w_out = to_local(fr, neg(rd));
+    f3 wi;
+    float pdf;
+    f3 fv = sample_f(M, g, w_out, &wi, &pdf);
+    f3 wi_world = normalize(to_world(fr, wi));
+    float cp = dot(prev_n, rd);
+    Vtx v;
+    v.alpha = divs(mul(muls(prev_alpha, fabsf(cp)), prev_f), prev_pdf);
+    v.pos = hit_p;
+    v.n = n;
+    v.zh = fr.Z;
+    v.mat = mat;
+    v.woz = 0; v.fwd = 1; v.q = 0; v.revg = 0;
+    out[count++] = v;
+    if (i >= max_depth + 1 || count >= MAXV) break;
+    ro = hit_p; rd = wi_world; rmin = BDPT_EPS_F; rmax = INFINITY;
+    prev_f = fv;
+    prev_n = n;
+    prev_pdf = pdf * 1.0f;
+    prev_alpha = v.alpha;
+    i++;
+  }
+  return count;
+}
+
+// MIS step quantities between a vertex `cur` and a neighbour `oth` whose BSDF/frame is used:
+// d = normalize(cur - oth), g = |(w2o(oth)*d).z * dot(d, cur.n)| / dist^2 (bidirection.cpp:151-158).
+BDPT_HD float step_g(f3 cur_pos, f3 cur_n, f3 oth_pos, f3 oth_zh, f3* dw_out) {
+  f3 dw = sub(cur_pos, oth_pos);
+  float dist = norm(dw);
+  dw = normalize(dw);
+  float wz = lz(dw, oth_zh);
+  *dw_out = dw;
+  return fabsf(wz * dot(dw, cur_n)) / (dist * dist);
+}
+
+// Per-subpath MIS constants (see Vtx).
+template <int MAXV>
+BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
+  const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
+  int nh = P.nE - 2;
+  for (int k = 0; k < nh; k++) {   // vertex E[k+2]
+    Vtx& v = P.E[k];
+    f3 prevp = k == 0 ? cam : P.E[k - 1].pos;
+    v.woz = lz(normalize(sub(prevp, v.pos)), v.zh);
+    if (k == 0) {
+      v.fwd = 1.0f * 1.0f;
+    } else {
+      const Vtx& nx = P.E[k - 1];
+      f3 dw;
+      float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
+      float p = pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
+      v.fwd = p * g2;
+    }
+  }
+  for (int k = 0; k + 1 < nh; k++) {
+    Vtx& v = P.E[k];
+    const Vtx& pv = P.E[k + 1];
+    f3 dw;
+    float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+    float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
+    v.revg = g;
+    v.q = (p * g) / v.fwd;
+  }
+}
+
+template <int MAXV>
+BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
+  int nv = P.nL - 1;   // L[1..nL-1]
+  for (int k = 0; k < nv; k++) {   // vertex L[k+1]
+    Vtx& v = P.L[k];
+    if (k == 0) {
+      v.fwd = l1_p;
+      v.woz = 0;
+      continue;
+    }
+    const Vtx& nx = P.L[k - 1];
+    v.woz = lz(normalize(sub(nx.pos, v.pos)), v.zh);
+    f3 dw;
+    float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
+    float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
+    v.fwd = p * g2;
+  }
+  for (int k = 0; k + 1 < nv; k++) {
+    Vtx& v = P.L[k];
+    const Vtx& pv = P.L[k + 1];
+    f3 dw;
+    float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+    float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
+    v.revg = g;
+    v.q = (p * g) / v.fwd;
+  }
+}
+
+// AreaLight/PointLight BDPT methods (light.cpp:115-153, 219-284).
+BDPT_HD bool light_contains(const DLight& l, f3 p) {
+  f3 lp = mk3(l.pos[0], l.pos[1], l.pos[2]);
+  if (l.type == LIGHT_POINT) return norm(sub(p, lp)) < BDPT_EPS_F;
+  f3 d = normalize(sub(lp, p));
+  return fabsf(dot(d, mk3(l.dir[0], l.dir[1], l.dir[2]))) < BDPT_EPS_F;
+}
+// sample_pdf's dir_pdf for a point known to be on the light; wi = direction of travel.
+BDPT_HD float light_dir_pdf(const DLight& l, f3 wi) {
+  if (l.type == LIGHT_POINT) return 0.25f / BDPT_PI_F;
+  Frame f;
+  f.X = mk3(l.fx[0], l.fx[1], l.fx[2]);
+  f.Y = mk3(l.fy[0], l.fy[1], l.fy[2]);
+  f.Z = mk3(l.fz[0], l.fz[1], l.fz[2]);
+  f3 wl = normalize(to_local(f, neg(wi)));
+  return cosine_pdf_z(wl.z);
+}
+
+BDPT_HD LightSample light_sample_point(const DLight& l, int nlights, Rng& g, f3 p, float* lpp_out) {
+  LightSample s;
+  f3 rad = mk3(l.rad[0], l.rad[1], l.rad[2]);
+  f3 dirv = mk3(l.dir[0], l.dir[1], l.dir[2]);
+  float lpp;
+  if (l.type == LIGHT_POINT) {
+    f3 lp = mk3(l.pos[0], l.pos[1], l.pos[2]);
+    f3 d = sub(lp, p);
+    f3 wi = normalize(d);
+    lpp = 1.0f;
+    s.dir_pdf = 0.25f / BDPT_PI_F;
+    s.n = neg(wi);
+    s.pos = lp;
+  } else {
+    float sx, sy;
+    grid2d(g, &sx, &sy);
+    sx = sx - 0.5f;
+    sy = sy - 0.5f;
+    f3 pt = add(add(mk3(l.pos[0], l.pos[1], l.pos[2]), smul(sx, mk3(l.dx[0], l.dx[1], l.dx[2]))),
+                smul(sy, mk3(l.dy[0], l.dy[1], l.dy[2])));
+    f3 d = sub(pt, p);
+    float cosT = dot(d, dirv);
+    float dd = sqrtf(norm2(d));
+    f3 wi = divs(d, dd);
+    lpp = 1.0f / l.area;
+    s.n = dirv;
+    s.pos = pt;
+    s.dir_pdf = cosine_pdf_z(lz(neg(wi), mk3(l.fz[0], l.fz[1], l.fz[2])));
+    if (!(cosT < 0)) rad = splat3(0);
+  }
+  lpp = lpp / (float)nlights;
+  s.alpha = divs(rad, lpp);
+  s.zh = zaxis(s.n);
+  *lpp_out = lpp;
+  return s;
+}
+
+// Camera::generate_ray (camera.cpp:191-212)
+BDPT_HD f3 camera_dir(const DCam& c, float x, float y) {
+  float rx = (2 * x - 1) * c.tanh_;
+  float ry = (2 * y - 1) * c.tanv_;
+  float rz = -1;
+  f3 w = add(add(smul(rx, mk3(c.c2w[0], c.c2w[1], c.c2w[2])), smul(ry, mk3(c.c2w[3], c.c2w[4], c.c2w[5]))),
+             smul(rz, mk3(c.c2w[6], c.c2w[7], c.c2w[8])));
+  return normalize(w);
+}
+
+struct EyeSample {
+  f3 pos, n, zh, alpha;
+  float dir_pdf;
+  int x, y;
+};
+// Camera::sample_ray_pdf (camera.cpp:214-248) with cos(acos z) = z.
+BDPT_HD EyeSample camera_sample(const DCam& c, int W, int H, f3 p) {
+  EyeSample e;
+  f3 cam = mk3(c.pos[0], c.pos[1], c.pos[2]);
+  f3 wi = sub(cam, p);
+  float dist = norm(wi);
+  wi = normalize(wi);
+  f3 mw = neg(wi);
+  f3 wc = add(add(smul(mw.x, mk3(c.w2c[0], c.w2c[1], c.w2c[2])), smul(mw.y, mk3(c.w2c[3], c.w2c[4], c.w2c[5]))),
+              smul(mw.z, mk3(c.w2c[6], c.w2c[7], c.w2c[8])));
+  wc.z = -wc.z;
+  float ct = wc.z;
+  float c2 = ct * ct;
+  float denom = 4 * c.tanh_ * c.tanv_ / (c2 * c2);
+  e.dir_pdf = (dist * dist) / ct;
+  e.n = neg(wi);
+  float rz = 1.0f / wc.z;
+  wc = mk3(wc.x * rz, wc.y * rz, wc.z * rz);
+  float fx = ((wc.x / c.tanh_ + 1) * 0.5f) * (float)W;
+  float fy = ((wc.y / c.tanv_ + 1) * 0.5f) * (float)H;
+  e.x = (fx > -1.0f && fx < (float)W) ? (int)fx : -1;
+  e.y = (fy > -1.0f && fy < (float)H) ? (int)fy : -1;
+  e.alpha = divs(splat3(1.0f / denom), 1.0f);
+  e.pos = cam;
+  e.zh = zaxis(e.n);
+  return e;
+}
+
+BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
+
+// multiple_importance_sampling_weight (bidirection.cpp:121-293) with cached path constants.
+// i, j: reference vertex indices; vs: connection endpoint on the light side for the eye walk
+// (LS for j == 1, L[j] otherwise); es: camera sample for i == 1.
+template <int MAXV>
+BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j, const LightSample& ls,
+                         const EyeSample& es, int eye_light) {
+  float w_inv = 0.0f, ratio = 1.0f;
+  w_inv += ratio;
+  if (i >= 2) {
+    const Vtx& cur = P.E[i - 2];
+    float nom;
+    if (j == 0) {
+      float p = 1.0f / S.lights[eye_light].area;
+      if (S.lights[eye_light].type == LIGHT_POINT) p = 1.0f;
+      nom = p * 1.0f;
+    } else {
+      f3 ppos = j == 1 ? ls.pos : P.L[j - 1].pos;
+      f3 pzh = j == 1 ? ls.zh : P.L[j - 1].zh;
+      f3 dw;
+      float g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+      float p = j == 1 ? ls.dir_pdf * 1.0f
+                       : pdf_b(S.mats[P.L[j - 1].mat], P.L[j - 1].n, pzh, dw) * 1.0f;
+      nom = p * g;
+    }
+    ratio *= nom / cur.fwd;
+    int prev_mat = i == 2 ? -1 : P.E[i - 3].mat;
+    bool dl = is_delta(S.mats[cur.mat].type) || (prev_mat >= 0 && is_delta(S.mats[prev_mat].type));
+    if (!dl) w_inv += ratio * ratio;
+    for (int k = i - 1; k >= 2; k--) {
+      const Vtx& v = P.E[k - 2];
+      float q;
+      if (j == 0 && k == i - 1) {
+        f3 dw = normalize(sub(v.pos, cur.pos));
+        float dp = light_dir_pdf(S.lights[eye_light], neg(dw));
+        q = ((dp * 1.0f) * v.revg) / v.fwd;
+      } else {
+        q = v.q;
+      }
+      ratio *= q;
+      int pm = k == 2 ? -1 : P.E[k - 3].mat;
+      bool d2 = is_delta(S.mats[v.mat].type) || (pm >= 0 && is_delta(S.mats[pm].type));
+      if (!d2) w_inv += ratio * ratio;
+    }
+  }
+  ratio = 1.0f;
+  if (j >= 1) {
+    const Vtx& cur = P.L[j - 1];
+    f3 ppos = i == 1 ? es.pos : P.E[i - 2].pos;
+    f3 pzh = i == 1 ? es.zh : P.E[i - 2].zh;
+    f3 dw;
+    float g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+    float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[P.E[i - 2].mat], P.E[i - 2].n, pzh, dw) * 1.0f;
+    float nom = p * g;
+    ratio *= nom / cur.fwd;
+    int prev_mat = j == 1 ? -1 : P.L[j - 2].mat;
+    bool dl = (cur.mat >= 0 && is_delta(S.mats[cur.mat].type)) || (prev_mat >= 0 && is_delta(S.mats[prev_mat].type));
+    if (!dl) w_inv += ratio * ratio;
+    for (int k = j - 1; k >= 1; k--) {
+      const Vtx& v = P.L[k - 1];
+      ratio *= v.q;
+      int pm = k == 1 ? -1 : P.L[k - 2].mat;
+      bool d2 = (v.mat >= 0 && is_delta(S.mats[v.mat].type)) || (pm >= 0 && is_delta(S.mats[pm].type));
+      if (!d2) w_inv += ratio * ratio;
+    }
+  }
+  return 1.0f / w_inv;
+}
+
+// One pixel-sample: est_radiance_global_illumination (bidirection.cpp:472-500) with the
+// connection loop estimate_bidirection_radiance (:296-469). Returns the eye-image value;
+// light-image splats (t = 1) go to sink.splat(x, y, value / spp).
+template <int MAXV, class Sink>
+BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt,
+                         int x, int y, uint32_t sample, Sink& sink) {
+  Rng g;
+  rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
+  // raytrace_pixel (bidirection.cpp:515-524)
+  float px, py;
+  grid2d(g, &px, &py);
+  px = px + (float)x;
+  py = py + (float)y;
+  float dx = px / (float)sp.W, dy = py / (float)sp.H;
+  const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
+  f3 rd = camera_dir(S.cam, dx, dy);
+  // eye subpath
+  int ne = random_walk<MAXV>(S, g, cnt, cam, rd, S.cam.nclip, S.cam.fclip, 1.0f, 1.0f, splat3(1.0f), rd,
+                             sp.max_depth, P.E);
+  P.nE = ne + 2;
+  // light subpath (sample_light_ray, bidirection.cpp:105-118)
+  int lid = (int)(rng_next(g) * (float)S.nlights);
+  if (lid >= S.nlights) lid = S.nlights - 1;
+  const DLight& L0 = S.lights[lid];
+  f3 lo, ld, ln;
+  float lpp, ldp;
+  f3 lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
+  if (L0.type == LIGHT_POINT) {
+    float z = rng_next(g) * 2 - 1;
+    float sinT = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+    float u = rng_next(g);
+    float c, s;
+    cos_sin_2pi(u, &c, &s);
+    ld = mk3(c * sinT, s * sinT, z);
+    lo = mk3(L0.pos[0], L0.pos[1], L0.pos[2]);
+    lpp = 1;
+    ldp = 0.25f / BDPT_PI_F;
+    ln = ld;
+  } else {
+    float sx, sy;
+    grid2d(g, &sx, &sy);
+    sx = sx - 0.5f;
+    sy = sy - 0.5f;
+    lo = add(add(mk3(L0.pos[0], L0.pos[1], L0.pos[2]), smul(sx, mk3(L0.dx[0], L0.dx[1], L0.dx[2]))),
+             smul(sy, mk3(L0.dy[0], L0.dy[1], L0.dy[2])));
+    f3 dl = cosine_hemi(g, &ldp);
+    Frame lf;
+    lf.X = mk3(L0.fx[0], L0.fx[1], L0.fx[2]);
+    lf.Y = mk3(L0.fy[0], L0.fy[1], L0.fy[2]);
+    lf.Z = mk3(L0.fz[0], L0.fz[1], L0.fz[2]);
+    ld = to_world(lf, dl);
+    lpp = 1.0f / L0.area;
+    ln = mk3(L0.dir[0], L0.dir[1], L0.dir[2]);
+  }
+  lpp = lpp / (float)S.nlights;
+  {
+    Vtx& v1 = P.L[0];
+    v1.pos = lo;
+    v1.n = ln;
+    v1.zh = zaxis(ln);
+    v1.alpha = divs(lrad, lpp);
+    v1.mat = -1;
+    v1.q = 0; v1.revg = 0; v1.woz = 0;
+  }
+  P.l1_dir_pdf = ldp;
+  int nl = random_walk<MAXV>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1);
+  P.nL = nl + 2;
+  eye_constants<MAXV>(S, P);
+  light_constants<MAXV>(S, P, lpp);
+
+  const float inv_spp = 1.0f / (float)sp.spp;
+  f3 eye_sum = splat3(0);
+  for (int i = 1; i < P.nE; i++) {
+    const bool eye_cam = i == 1;
+    const Vtx* ev = eye_cam ? nullptr : &P.E[i - 2];
+    const f3 epos = eye_cam ? cam : ev->pos;
+    for (int j = 0; j < P.nL; j++) {
+      LightSample ls;
+      EyeSample es;
+      es.x = -1; es.y = -1;
+      f3 c = splat3(0);
+      int eye_light = -1;
+      if (j == 0) {
+        if (eye_cam) continue;
+        const DMat& M = S.mats[ev->mat];
+        if (M.type != MAT_EMISSION) continue;
+        c = mk3(M.a[0], M.a[1], M.a[2]);
+        if (!(norm(c) > BDPT_EPS_F)) continue;
+        for (int l = 0; l < S.nlights; l++)
+          if (light_contains(S.lights[l], ev->pos)) { eye_light = l; break; }
+        if (eye_light < 0) continue;
+        f3 prevp = i == 2 ? cam : P.E[i - 3].pos;
+        f3 wi = normalize(sub(ev->pos, prevp));
+        const DLight& EL = S.lights[eye_light];
+        if (!(light_dir_pdf(EL, wi) > 0)) continue;
+        c = mk3(EL.rad[0], EL.rad[1], EL.rad[2]);
+        f3 contrib = mul(mul(ev->alpha, splat3(1.0f)), c);
+        float w = 0;
+        if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, 0, ls, es, eye_light);
+        eye_sum = add(eye_sum, muls(contrib, w));
+        continue;
+      }
+      // f_light / vl
+      f3 vl_pos, vl_n, la;
+      if (j == 1) {
+        int id = (int)(rng_next(g) * (float)S.nlights);
+        if (id >= S.nlights) id = S.nlights - 1;
+        float lp;
+        ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
+        vl_pos = ls.pos; vl_n = ls.n; la = ls.alpha;
+      } else {
+        const Vtx& lv = P.L[j - 1];
+        vl_pos = lv.pos; vl_n = lv.n; la = lv.alpha;
+      }
+      f3 ve_pos, ve_n, ea;
+      if (eye_cam) {
+        es = camera_sample(S.cam, sp.W, sp.H, vl_pos);
+        ve_pos = es.pos; ve_n = es.n; ea = es.alpha;
+      } else {
+        ve_pos = ev->pos; ve_n = ev->n; ea = ev->alpha;
+      }
+      f3 f_eye = splat3(1.0f), f_light = splat3(1.0f);
+      if (!eye_cam) {
+        const DMat& M = S.mats[ev->mat];
+        float cz = lz(normalize(sub(vl_pos, ev->pos)), ev->zh);
+        if (M.type != MAT_DIFFUSE || ev->woz < 0 || cz < 0) continue;   // f_eye = 0
+        f_eye = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
+      }
+      if (j >= 2) {
+        const Vtx& lv = P.L[j - 1];
+        const DMat& M = S.mats[lv.mat];
+        float cz = lz(normalize(sub(ve_pos, lv.pos)), lv.zh);
+        if (M.type != MAT_DIFFUSE || cz < 0 || lv.woz < 0) continue;   // f_light = 0
+        f_light = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
+      }
+      f3 eal = mul(ea, la);
+      if (!nonzero3(eal)) continue;
+      f3 conn = sub(vl_pos, ve_pos);
+      float dist = norm(conn);
+      conn = normalize(conn);
+      if (trace_any(S, ve_pos, conn, BDPT_EPS_F, dist - BDPT_EPS_F, cnt)) continue;
+      float gg = fabsf(dot(vl_n, conn) * dot(ve_n, conn)) / (dist * dist);
+      c = mul(muls(f_eye, gg), f_light);
+      f3 contrib = mul(eal, c);
+      float w = 0;
+      if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, j, ls, es, -1);
+      f3 ill = muls(contrib, w);
+      if (eye_cam) {
+        if (es.x >= 0 && es.y >= 0 && es.x < sp.W && es.y < sp.H) sink.splat(es.x, es.y, divs(ill, (float)sp.spp));
+      } else {
+        eye_sum = add(eye_sum, ill);
+      }
+    }
+  }
+  (void)inv_spp;
+  return eye_sum;
+}
+
+}  // namespace bdpt

@@ -1,0 +1,457 @@
+// bdpt_hip.hip — HIP kernels for gfx950 + the C-ABI of include/bdpt/bdpt.h (libbdpt_amd.so).
+//
+// k_bdpt_sample: one lane per (pixel, chunk of samples). Lanes of a wave cover an 8x8 pixel block
+// at the same sample index (coherent primary rays and BVH paths). Each lane runs the reference's
+// per-sample estimator (bdpt_core.h: eye walk, light walk, all s x t connections with MIS),
+// accumulates its eye-image value in registers and adds it once per chunk to the fp32 eye frame;
+// t = 1 light-tracing splats (bidirection.cpp:457-466) are fp32 atomics into the light frame —
+// the device form of update_pixel under update_lock (bidirection.cpp:544-551).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see __graft_entry__.build).
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bdpt/bdpt.h"
+#include "bdpt_core.h"
+#include "bdpt_scene.h"
+
+using namespace bdpt;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct KParams {
+  SceneView S;
+  SampleParams sp;
+  float* eye;        // W*H*3
+  float* light;      // W*H*3
+  unsigned long long* stats;  // 8 counters
+  const int4* blocks;         // tile blocks (x0, y0, w, h) of <= 8x8 pixels; null = full frame
+  int nblocks;
+  int nbx;                    // full-frame: blocks per row
+  int spp_begin, spp_end, spl;
+  long long lanes_per_chunk;
+  long long nlanes;
+};
+
+struct DevSink {
+  float* light;
+  int W;
+  __device__ void splat(int x, int y, f3 v) {
+    float* p = light + 3 * ((size_t)x + (size_t)y * W);
+    atomicAdd(p, v.x);
+    atomicAdd(p + 1, v.y);
+    atomicAdd(p + 2, v.z);
+  }
+};
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int MAXV, bool STATS>
+__global__ __launch_bounds__(128) void k_bdpt_sample(KParams kp) {
+  const long long lane = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  unsigned nsamp = 0;
+  if (lane < kp.nlanes) {
+    const long long chunk = lane / kp.lanes_per_chunk;
+    const long long within = lane - chunk * kp.lanes_per_chunk;
+    const int blk = (int)(within >> 6), q = (int)(within & 63);
+    int bx0, by0, bw, bh;
+    if (kp.blocks) {
+      int4 b = kp.blocks[blk];
+      bx0 = b.x; by0 = b.y; bw = b.z; bh = b.w;
+    } else {
+      bx0 = (blk % kp.nbx) * 8;
+      by0 = (blk / kp.nbx) * 8;
+      bw = min(8, kp.sp.W - bx0);
+      bh = min(8, kp.sp.H - by0);
+    }
+    const int qx = q & 7, qy = q >> 3;
+    if (qx < bw && qy < bh) {
+      const int x = bx0 + qx, y = by0 + qy;
+      const int s0 = kp.spp_begin + (int)chunk * kp.spl;
+      const int s1 = min(s0 + kp.spl, kp.spp_end);
+      Paths<MAXV> P;
+      DevSink sink{kp.light, kp.sp.W};
+      const float inv = 1.0f / (float)kp.sp.spp;
+      float ax = 0, ay = 0, az = 0;
+      for (int s = s0; s < s1; s++) {
+        f3 v = render_sample<MAXV>(kp.S, kp.sp, P, cnt, x, y, (uint32_t)s, sink);
+        ax += v.x * inv;
+        ay += v.y * inv;
+        az += v.z * inv;
+        nsamp++;
+      }
+      float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
+      if (ax != 0) atomicAdd(e, ax);
+      if (ay != 0) atomicAdd(e + 1, ay);
+      if (az != 0) atomicAdd(e + 2, az);
+    }
+  }
+  if (STATS) {
+    unsigned v[7] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      unsigned s = wave_sum(v[k]);
+      if ((threadIdx.x & 63) == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
+    }
+  }
+}
+
+__global__ void k_trace_rays(SceneView S, const float* rays, int n, int any_hit, float* out_t, int* out_prim,
+                             const int* prim_ref) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* r = rays + 8 * (size_t)i;
+  f3 o = mk3(r[0], r[1], r[2]), d = mk3(r[3], r[4], r[5]);
+  Counters c = {0, 0, 0, 0, 0, 0};
+  if (any_hit) {
+    bool h = trace_any(S, o, d, r[6], r[7], c);
+    out_t[i] = h ? 0.0f : INFINITY;
+    out_prim[i] = h ? 0 : -1;
+  } else {
+    Hit h;
+    bool ok = trace_closest(S, o, d, r[6], r[7], h, c);
+    out_t[i] = ok ? h.t : INFINITY;
+    out_prim[i] = ok ? prim_ref[h.prim] : -1;
+  }
+}
+
+__global__ void k_combine(const float* a, const float* b, float* out, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+struct Ctx {
+  HostScene hs;
+  bdpt_params prm;
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  float* d_nodes = nullptr;
+  float* d_geom = nullptr;
+  float* d_shade = nullptr;
+  DMat* d_mats = nullptr;
+  DLight* d_lights = nullptr;
+  int* d_prim_ref = nullptr;
+  float* d_eye = nullptr;
+  float* d_light = nullptr;
+  float* d_sample = nullptr;
+  unsigned long long* d_stats = nullptr;
+  int4* d_blocks = nullptr;
+  size_t blocks_cap = 0;
+  int4* h_blocks = nullptr;   // pinned staging
+  size_t h_blocks_cap = 0;
+  int maxv = 5;
+  size_t npix = 0;
+};
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return BDPT_E_DEVICE;                                                         \
+    }                                                                               \
+  } while (0)
+
+SceneView view_of(const Ctx* c) {
+  SceneView S;
+  S.nodes = (const float4*)c->d_nodes;
+  S.geom = (const float4*)c->d_geom;
+  S.shade = (const float4*)c->d_shade;
+  S.mats = c->d_mats;
+  S.lights = c->d_lights;
+  S.nlights = (int)c->hs.lights.size();
+  S.root = c->hs.root;
+  S.cam = c->hs.cam;
+  return S;
+}
+
+template <int MAXV>
+int launch_maxv(Ctx* c, KParams& kp, unsigned grid) {
+  if (c->prm.collect_stats)
+    hipLaunchKernelGGL((k_bdpt_sample<MAXV, true>), dim3(grid), dim3(128), 0, c->stream, kp);
+  else
+    hipLaunchKernelGGL((k_bdpt_sample<MAXV, false>), dim3(grid), dim3(128), 0, c->stream, kp);
+  HIPCHK(hipGetLastError());
+  return BDPT_OK;
+}
+
+void free_ctx(Ctx* c) {
+  if (!c) return;
+  void* bufs[] = {c->d_nodes, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref,
+                  c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->h_blocks) (void)hipHostFree(c->h_blocks);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+template <class T>
+int upload(T** dst, const std::vector<T>& v) {
+  size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
+  HIPCHK(hipMalloc((void**)dst, bytes));
+  if (!v.empty()) HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return BDPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdpt_abi_version(void) { return BDPT_ABI_VERSION; }
+const char* bdpt_last_error(void) { return g_err.c_str(); }
+
+int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** ctx_out) {
+  if (!scene || !params || !ctx_out) { g_err = "null argument"; return BDPT_E_INVALID; }
+  *ctx_out = nullptr;
+  const bdpt_params& p = *params;
+  if (p.width <= 0 || p.height <= 0 || p.spp <= 0 || p.max_depth < 0) {
+    g_err = "invalid frame size / spp / max_depth";
+    return BDPT_E_INVALID;
+  }
+  int need = p.max_depth < 1 ? 1 : p.max_depth;
+  if (need > 16) { g_err = "max_depth > 16 not compiled"; return BDPT_E_UNSUPPORTED; }
+  Ctx* c = new Ctx();
+  c->prm = p;
+  c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : 16;
+  int rc = build_host_scene(scene, c->hs, g_err);
+  if (rc) { delete c; return rc; }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    g_err = "no HIP device";
+    delete c;
+    return BDPT_E_DEVICE;
+  }
+  if (p.device < 0 || p.device >= ndev) { g_err = "bad device ordinal"; delete c; return BDPT_E_INVALID; }
+  c->device = p.device;
+  auto fail = [&](int code) { free_ctx(c); return code; };
+  if (hipSetDevice(c->device) != hipSuccess) { g_err = "hipSetDevice failed"; return fail(BDPT_E_DEVICE); }
+  if ((rc = upload(&c->d_nodes, c->hs.nodes))) return fail(rc);
+  if ((rc = upload(&c->d_geom, c->hs.geom))) return fail(rc);
+  if ((rc = upload(&c->d_shade, c->hs.shade))) return fail(rc);
+  if ((rc = upload(&c->d_mats, c->hs.mats))) return fail(rc);
+  if ((rc = upload(&c->d_lights, c->hs.lights))) return fail(rc);
+  if ((rc = upload(&c->d_prim_ref, c->hs.prim_ref))) return fail(rc);
+  c->npix = (size_t)p.width * p.height;
+  size_t fb = c->npix * 3 * sizeof(float);
+  if (hipMalloc((void**)&c->d_eye, fb) != hipSuccess || hipMalloc((void**)&c->d_light, fb) != hipSuccess ||
+      hipMalloc((void**)&c->d_sample, fb) != hipSuccess ||
+      hipMalloc((void**)&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    g_err = "out of device memory";
+    return fail(BDPT_E_NOMEM);
+  }
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    g_err = "stream/event creation failed";
+    return fail(BDPT_E_DEVICE);
+  }
+  c->stream = c->own;
+  if (hipMemsetAsync(c->d_eye, 0, fb, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_light, 0, fb, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) { g_err = "init sync failed"; return fail(BDPT_E_DEVICE); }
+  *ctx_out = c;
+  return BDPT_OK;
+}
+
+void bdpt_destroy(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_ctx(c);
+}
+
+int bdpt_set_stream(void* ctx, void* stream) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return BDPT_OK;
+}
+
+int bdpt_clear(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  size_t fb = c->npix * 3 * sizeof(float);
+  HIPCHK(hipMemsetAsync(c->d_eye, 0, fb, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_light, 0, fb, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream));
+  return BDPT_OK;
+}
+
+int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_begin, int32_t spp_count) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  if (spp_begin < 0 || spp_count < 0 || ntiles < 0) { g_err = "negative argument"; return BDPT_E_INVALID; }
+  if (spp_count == 0) return BDPT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const int W = c->prm.width, H = c->prm.height;
+  KParams kp;
+  kp.S = view_of(c);
+  kp.sp.W = W; kp.sp.H = H; kp.sp.spp = c->prm.spp; kp.sp.max_depth = c->prm.max_depth; kp.sp.seed = c->prm.seed;
+  kp.eye = c->d_eye;
+  kp.light = c->d_light;
+  kp.stats = c->d_stats;
+  kp.blocks = nullptr;
+  kp.nbx = (W + 7) / 8;
+  kp.nblocks = kp.nbx * ((H + 7) / 8);
+  if (tiles && ntiles > 0) {
+    // Tiles (raytrace_tile clips them to the frame, raytraced_renderer.cpp:600-604) -> 8x8 blocks.
+    std::vector<int4> blk;
+    for (int t = 0; t < ntiles; t++) {
+      int x0 = std::max(0, tiles[t].x0), y0 = std::max(0, tiles[t].y0);
+      int x1 = std::min(W, tiles[t].x0 + tiles[t].w), y1 = std::min(H, tiles[t].y0 + tiles[t].h);
+      for (int by = y0; by < y1; by += 8)
+        for (int bx = x0; bx < x1; bx += 8) blk.push_back(make_int4(bx, by, std::min(8, x1 - bx), std::min(8, y1 - by)));
+    }
+    if (blk.empty()) return BDPT_OK;
+    if (blk.size() > c->blocks_cap) {
+      HIPCHK(hipStreamSynchronize(c->stream));
+      if (c->d_blocks) (void)hipFree(c->d_blocks);
+      if (c->h_blocks) (void)hipHostFree(c->h_blocks);
+      c->blocks_cap = blk.size();
+      HIPCHK(hipMalloc((void**)&c->d_blocks, c->blocks_cap * sizeof(int4)));
+      HIPCHK(hipHostMalloc((void**)&c->h_blocks, c->blocks_cap * sizeof(int4)));
+    } else {
+      HIPCHK(hipStreamSynchronize(c->stream));   // staging buffer reuse
+    }
+    memcpy(c->h_blocks, blk.data(), blk.size() * sizeof(int4));
+    HIPCHK(hipMemcpyAsync(c->d_blocks, c->h_blocks, blk.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    kp.blocks = c->d_blocks;
+    kp.nblocks = (int)blk.size();
+  }
+  int spl = c->prm.samples_per_lane;
+  if (spl <= 0) {
+    // enough lanes to fill 256 CUs several times over, but >= 1 sample per lane
+    long long pix_lanes = (long long)kp.nblocks * 64;
+    long long want = 256LL * 2048;
+    spl = (int)std::max(1LL, std::min<long long>(spp_count, (pix_lanes * spp_count) / want));
+  }
+  kp.spl = spl;
+  kp.spp_begin = spp_begin;
+  kp.spp_end = spp_begin + spp_count;
+  int nchunks = (spp_count + spl - 1) / spl;
+  kp.lanes_per_chunk = (long long)kp.nblocks * 64;
+  kp.nlanes = kp.lanes_per_chunk * nchunks;
+  long long grid = (kp.nlanes + 127) / 128;
+  if (grid > 0x7fffffff) { g_err = "launch too large; split spp"; return BDPT_E_INVALID; }
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  int rc = c->maxv == 5 ? launch_maxv<5>(c, kp, (unsigned)grid)
+         : c->maxv == 8 ? launch_maxv<8>(c, kp, (unsigned)grid)
+                        : launch_maxv<16>(c, kp, (unsigned)grid);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  return BDPT_OK;
+}
+
+int bdpt_sync(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return BDPT_OK;
+}
+
+int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !dptr) { g_err = "null argument"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  if (which == BDPT_FRAME_EYE) { *dptr = c->d_eye; return BDPT_OK; }
+  if (which == BDPT_FRAME_LIGHT) { *dptr = c->d_light; return BDPT_OK; }
+  if (which != BDPT_FRAME_SAMPLE) { g_err = "bad frame id"; return BDPT_E_INVALID; }
+  long long n = (long long)c->npix * 3;
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->d_eye, c->d_light,
+                     c->d_sample, n);
+  HIPCHK(hipGetLastError());
+  *dptr = c->d_sample;
+  return BDPT_OK;
+}
+
+int bdpt_copy_frame(void* ctx, int32_t which, void* dst_device) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !dst_device) { g_err = "null argument"; return BDPT_E_INVALID; }
+  void* p = nullptr;
+  int rc = bdpt_frame_device_ptr(ctx, which, &p);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(dst_device, p, c->npix * 3 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+  return BDPT_OK;
+}
+
+int bdpt_read_frame(void* ctx, int32_t which, float* rgb) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !rgb) { g_err = "null argument"; return BDPT_E_INVALID; }
+  void* p = nullptr;
+  int rc = bdpt_frame_device_ptr(ctx, which, &p);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(rgb, p, c->npix * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return BDPT_OK;
+}
+
+int bdpt_get_stats(void* ctx, bdpt_stats* out) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !out) { g_err = "null argument"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned long long s[8];
+  HIPCHK(hipMemcpy(s, c->d_stats, sizeof s, hipMemcpyDeviceToHost));
+  memset(out, 0, sizeof *out);
+  out->samples = s[0];
+  out->closest_rays = s[1];
+  out->shadow_rays = s[2];
+  out->rays = s[1] + s[2];
+  out->node_visits = s[3];
+  out->tri_tests = s[4];
+  out->sph_tests = s[5];
+  out->hits = s[6];
+  float ms = 0;
+  if (c->timed) HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  out->last_kernel_ms = ms;
+  out->bvh_nodes = (uint64_t)c->hs.ref_nodes;
+  out->bvh_depth = (uint64_t)c->hs.depth;
+  return BDPT_OK;
+}
+
+int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, float* out_t, int32_t* out_prim) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || (!rays && n) || n < 0) { g_err = "bad argument"; return BDPT_E_INVALID; }
+  if (n == 0) return BDPT_OK;
+  HIPCHK(hipSetDevice(c->device));
+  float *d_r = nullptr, *d_t = nullptr;
+  int* d_p = nullptr;
+  HIPCHK(hipMalloc((void**)&d_r, (size_t)n * 8 * sizeof(float)));
+  HIPCHK(hipMalloc((void**)&d_t, (size_t)n * sizeof(float)));
+  HIPCHK(hipMalloc((void**)&d_p, (size_t)n * sizeof(int)));
+  HIPCHK(hipMemcpy(d_r, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_trace_rays, dim3((n + 127) / 128), dim3(128), 0, c->stream, view_of(c), d_r, n, any_hit,
+                     d_t, d_p, c->d_prim_ref);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out_t, d_t, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out_prim, d_p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipFree(d_r);
+  (void)hipFree(d_t);
+  (void)hipFree(d_p);
+  return BDPT_OK;
+}
+
+}  // extern "C"

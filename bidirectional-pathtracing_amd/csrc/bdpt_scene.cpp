@@ -1,0 +1,284 @@
+// bdpt_scene.cpp — host-side scene preparation (see bdpt_scene.h).
+#include "bdpt_scene.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace bdpt {
+
+namespace {
+
+struct Box {  // BBox (bbox.h:19-136), fp64
+  double mn[3], mx[3];
+  void from_point(const double* p) {
+    for (int k = 0; k < 3; k++) mn[k] = mx[k] = p[k];
+  }
+  void expand(const Box& b) {
+    for (int k = 0; k < 3; k++) {
+      mn[k] = std::min(mn[k], b.mn[k]);
+      mx[k] = std::max(mx[k], b.mx[k]);
+    }
+  }
+  void expand_pt(const double* p) {
+    for (int k = 0; k < 3; k++) {
+      mn[k] = std::min(mn[k], p[k]);
+      mx[k] = std::max(mx[k], p[k]);
+    }
+  }
+  double centroid(int k) const { return 0.5 * (mn[k] + mx[k]); }   // (min + max) / 2
+};
+
+struct Node {
+  int l = -1, r = -1;
+  int start = 0, count = 0;
+  Box box;
+};
+
+struct Builder {
+  const std::vector<Box>* pb;
+  std::vector<Node> nodes;
+  std::vector<int> leaf_prims;
+  int depth = 0;
+
+  int make_leaf(const std::vector<int>& prims) {
+    Node n;
+    n.box = (*pb)[prims[0]];
+    for (int p : prims) n.box.expand((*pb)[p]);
+    n.start = (int)leaf_prims.size();
+    n.count = (int)prims.size();
+    for (int p : prims) leaf_prims.push_back(p);
+    nodes.push_back(n);
+    return (int)nodes.size() - 1;
+  }
+
+  // construct_bvh (bvh.cpp:51-129). Where the reference asserts (no extent / empty side) the
+  // list is split in half in input order instead (documented divergence: the reference aborts).
+  int build(const std::vector<int>& prims, int d) {
+    depth = std::max(depth, d);
+    const auto& B = *pb;
+    if (prims.size() <= 4) return make_leaf(prims);
+    double xmax = 0, xmin = 0, ymax = 0, ymin = 0, zmax = 0, zmin = 0;
+    for (size_t i = 0; i < prims.size(); i++) {
+      const Box& b = B[prims[i]];
+      double cx = b.centroid(0), cy = b.centroid(1), cz = b.centroid(2);
+      xmax = i == 0 ? cx : std::max(xmax, cx);
+      xmin = i == 0 ? cx : std::min(xmin, cx);
+      ymax = i == 0 ? cy : std::max(ymax, cy);
+      ymin = i == 0 ? cy : std::min(ymin, cy);
+      zmax = i == 0 ? cz : std::max(zmax, cz);
+      zmin = i == 0 ? cz : std::min(zmin, cz);
+    }
+    double ranges[3] = {xmax - xmin, ymax - ymin, zmax - zmin};
+    double mins[3] = {xmin, ymin, zmin};
+    double max_range = std::max(ranges[0], std::max(ranges[1], ranges[2]));
+    int axis;
+    for (axis = 0; axis < 3; axis++)
+      if (ranges[axis] == max_range) break;
+    std::vector<int> left, right;
+    if (max_range > 0 && axis < 3) {
+      double mid = mins[axis] + ranges[axis] / 2;
+      for (int p : prims) {
+        if (B[p].centroid(axis) <= mid) left.push_back(p);
+        else right.push_back(p);
+      }
+    }
+    if (left.empty() || right.empty()) {
+      left.assign(prims.begin(), prims.begin() + prims.size() / 2);
+      right.assign(prims.begin() + prims.size() / 2, prims.end());
+    }
+    int id = (int)nodes.size();
+    nodes.push_back(Node());
+    int l = build(left, d + 1);
+    int r = build(right, d + 1);
+    Box bb = nodes[l].box;
+    bb.expand(nodes[r].box);
+    nodes[id].l = l;
+    nodes[id].r = r;
+    nodes[id].box = bb;
+    return id;
+  }
+};
+
+float pad_down(double v, double ext) {
+  double m = std::max(std::fabs(v), ext) * (1.0 / 65536.0) + 1e-30;
+  float f = (float)(v - m);
+  if ((double)f > v - m) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float pad_up(double v, double ext) {
+  double m = std::max(std::fabs(v), ext) * (1.0 / 65536.0) + 1e-30;
+  float f = (float)(v + m);
+  if ((double)f < v + m) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+float i2f(int v) {
+  float f;
+  std::memcpy(&f, &v, 4);
+  return f;
+}
+
+}  // namespace
+
+int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err) {
+  if (!d || d->nprim <= 0 || !d->prim_type || !d->prim_geom || !d->prim_mat) {
+    err = "scene has no primitives";
+    return BDPT_E_INVALID;
+  }
+  if (d->nmat <= 0 || !d->mats) { err = "scene has no materials"; return BDPT_E_INVALID; }
+  if (d->nlight <= 0 || !d->lights) { err = "scene has no light (BDPT needs one)"; return BDPT_E_INVALID; }
+  if (d->nprim >= (1 << 24)) { err = "too many primitives for the leaf encoding (2^24)"; return BDPT_E_INVALID; }
+  // materials (collada.cpp:854-938 -> bsdf.h classes)
+  out.mats.clear();
+  for (int i = 0; i < d->nmat; i++) {
+    const bdpt_material& m = d->mats[i];
+    if (m.type == BDPT_MAT_MICROFACET) {
+      err = "MicrofacetBSDF::sample_pdf is assert(0) under BDPT (advanced_bsdf.cpp:144-148)";
+      return BDPT_E_UNSUPPORTED;
+    }
+    if (m.type < BDPT_MAT_DIFFUSE || m.type > BDPT_MAT_REFRACTION) { err = "unknown material type"; return BDPT_E_INVALID; }
+    DMat M;
+    M.type = m.type;
+    for (int k = 0; k < 3; k++) { M.a[k] = (float)m.a[k]; M.b[k] = (float)m.b[k]; }
+    M.ior = (float)m.ior;
+    out.mats.push_back(M);
+  }
+  // lights (light.cpp:102-284)
+  out.lights.clear();
+  for (int i = 0; i < d->nlight; i++) {
+    const bdpt_light& l = d->lights[i];
+    if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT) {
+      err = "only area and point lights implement the BDPT light API (light.cpp:25-51,168-194,299-364)";
+      return BDPT_E_UNSUPPORTED;
+    }
+    DLight L;
+    std::memset(&L, 0, sizeof L);
+    L.type = l.type;
+    for (int k = 0; k < 3; k++) {
+      L.rad[k] = (float)l.radiance[k];
+      L.pos[k] = (float)l.position[k];
+      L.dir[k] = (float)l.direction[k];
+      L.dx[k] = (float)l.dim_x[k];
+      L.dy[k] = (float)l.dim_y[k];
+    }
+    L.area = (float)l.area;
+    Frame f = make_frame(mk3(L.dir[0], L.dir[1], L.dir[2]));
+    L.fx[0] = f.X.x; L.fx[1] = f.X.y; L.fx[2] = f.X.z;
+    L.fy[0] = f.Y.x; L.fy[1] = f.Y.y; L.fy[2] = f.Y.z;
+    L.fz[0] = f.Z.x; L.fz[1] = f.Z.y; L.fz[2] = f.Z.z;
+    out.lights.push_back(L);
+  }
+  // camera (camera.cpp:191-248): tan(hFov*PI/360) evaluated in fp64 then rounded
+  const bdpt_camera& c = d->camera;
+  const double PI_D = 3.14159265358979323;
+  for (int k = 0; k < 3; k++) out.cam.pos[k] = (float)c.pos[k];
+  for (int k = 0; k < 9; k++) { out.cam.c2w[k] = (float)c.c2w[k]; out.cam.w2c[k] = (float)c.w2c[k]; }
+  out.cam.tanh_ = (float)std::tan(c.hfov_deg * PI_D / 360);
+  out.cam.tanv_ = (float)std::tan(c.vfov_deg * PI_D / 360);
+  out.cam.nclip = (float)c.nclip;
+  out.cam.fclip = (float)c.fclip;
+
+  // primitive bboxes (triangle.cpp:9-21 / sphere.h:32-34)
+  const int n = d->nprim;
+  std::vector<Box> pb(n);
+  for (int i = 0; i < n; i++) {
+    const double* g = d->prim_geom + 18 * (size_t)i;
+    int m = d->prim_mat[i];
+    if (m < 0 || m >= d->nmat) { err = "primitive material index out of range"; return BDPT_E_INVALID; }
+    if (d->prim_type[i] == BDPT_PRIM_TRIANGLE) {
+      pb[i].from_point(g);
+      pb[i].expand_pt(g + 3);
+      pb[i].expand_pt(g + 6);
+    } else if (d->prim_type[i] == BDPT_PRIM_SPHERE) {
+      for (int k = 0; k < 3; k++) { pb[i].mn[k] = g[k] - g[3]; pb[i].mx[k] = g[k] + g[3]; }
+    } else {
+      err = "unknown primitive type";
+      return BDPT_E_INVALID;
+    }
+  }
+  Builder B;
+  B.pb = &pb;
+  std::vector<int> all(n);
+  for (int i = 0; i < n; i++) all[i] = i;
+  int root = B.build(all, 0);
+  out.depth = B.depth;
+  out.ref_nodes = (int)B.nodes.size();
+  out.nprim = n;
+  if (out.depth + 2 > BDPT_STACK) { err = "BVH deeper than the traversal stack"; return BDPT_E_UNSUPPORTED; }
+
+  // primitives in DFS leaf order
+  out.prim_ref = B.leaf_prims;
+  out.geom.assign(12 * (size_t)n, 0.0f);
+  out.shade.assign(12 * (size_t)n, 0.0f);
+  for (int k = 0; k < n; k++) {
+    int i = B.leaf_prims[k];
+    const double* g = d->prim_geom + 18 * (size_t)i;
+    float* G = &out.geom[12 * (size_t)k];
+    float* S = &out.shade[12 * (size_t)k];
+    if (d->prim_type[i] == BDPT_PRIM_TRIANGLE) {
+      float p1[3], p2[3], p3[3];
+      for (int c3 = 0; c3 < 3; c3++) { p1[c3] = (float)g[c3]; p2[c3] = (float)g[3 + c3]; p3[c3] = (float)g[6 + c3]; }
+      float e1[3], e2[3];
+      for (int c3 = 0; c3 < 3; c3++) { e1[c3] = p2[c3] - p1[c3]; e2[c3] = p3[c3] - p1[c3]; }
+      G[0] = p1[0]; G[1] = p1[1]; G[2] = p1[2]; G[3] = e1[0];
+      G[4] = e1[1]; G[5] = e1[2]; G[6] = e2[0]; G[7] = e2[1];
+      G[8] = e2[2];
+      for (int c3 = 0; c3 < 9; c3++) S[c3] = (float)g[9 + c3];
+      S[9] = i2f(d->prim_mat[i]);
+      S[10] = i2f(0);
+    } else {
+      G[0] = (float)g[0]; G[1] = (float)g[1]; G[2] = (float)g[2]; G[3] = (float)g[3];
+      S[9] = i2f(d->prim_mat[i]);
+      S[10] = i2f(1);
+    }
+  }
+  // nodes: pre-order over internal nodes; children refs
+  std::vector<int> dev_index(B.nodes.size(), -1);
+  std::vector<int> order;
+  {
+    std::vector<int> st;
+    if (B.nodes[root].l >= 0) st.push_back(root);
+    while (!st.empty()) {
+      int id = st.back();
+      st.pop_back();
+      dev_index[id] = (int)order.size();
+      order.push_back(id);
+      if (B.nodes[B.nodes[id].r].l >= 0) st.push_back(B.nodes[id].r);
+      if (B.nodes[B.nodes[id].l].l >= 0) st.push_back(B.nodes[id].l);
+    }
+  }
+  auto ref_of = [&](int id) -> int {
+    const Node& nd = B.nodes[id];
+    if (nd.l >= 0) return dev_index[id];
+    int mask = 0;
+    for (int k = 0; k < nd.count; k++) {
+      int i = B.leaf_prims[nd.start + k];
+      if (d->prim_type[i] == BDPT_PRIM_SPHERE) mask |= 1 << k;
+    }
+    uint32_t enc = ((uint32_t)nd.start << 7) | ((uint32_t)mask << 3) | (uint32_t)nd.count;
+    return (int)~enc;
+  };
+  out.nodes.assign(16 * order.size(), 0.0f);
+  for (size_t k = 0; k < order.size(); k++) {
+    const Node& nd = B.nodes[order[k]];
+    float* N = &out.nodes[16 * k];
+    const Box* cb[2] = {&B.nodes[nd.l].box, &B.nodes[nd.r].box};
+    float v[12];
+    for (int s = 0; s < 2; s++) {
+      const Box& b = *cb[s];
+      double ext = std::max(b.mx[0] - b.mn[0], std::max(b.mx[1] - b.mn[1], b.mx[2] - b.mn[2]));
+      for (int c3 = 0; c3 < 3; c3++) {
+        v[6 * s + c3] = pad_down(b.mn[c3], ext);
+        v[6 * s + 3 + c3] = pad_up(b.mx[c3], ext);
+      }
+    }
+    for (int c3 = 0; c3 < 12; c3++) N[c3] = v[c3];
+    N[12] = i2f(ref_of(nd.l));
+    N[13] = i2f(ref_of(nd.r));
+  }
+  out.root = ref_of(root);
+  return BDPT_OK;
+}
+
+}  // namespace bdpt

@@ -1,0 +1,41 @@
+// bdpt_scene.h — host-side scene preparation for the device path.
+//
+// Replaces RaytracedRenderer::build_accel (raytraced_renderer.cpp:350-374) + BVHAccel's
+// construct_bvh (bvh.cpp:51-129): the BVH topology is the reference's (longest centroid axis,
+// spatial midpoint, leaf <= 4, stable partition, built in fp64 on the reference's bboxes), then
+// flattened for HBM:
+//   nodes : 64 B per internal node = both children's fp32 AABBs (outward-rounded and padded by
+//           2^-16 of the box scale, so the fp32 slab test is conservative) + two child refs
+//   geom  : 48 B per primitive in DFS leaf order (triangle p0,e1,e2 | sphere c,r)
+//   shade : 48 B per primitive (triangle n1,n2,n3 | sphere flag) + material id
+//   prim_ref: DFS position -> reference primitive index
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "bdpt/bdpt.h"
+#include "bdpt_core.h"
+
+namespace bdpt {
+
+struct HostScene {
+  std::vector<float> nodes;   // 16 floats per node
+  std::vector<float> geom;    // 12 floats per prim
+  std::vector<float> shade;   // 12 floats per prim
+  std::vector<int32_t> prim_ref;
+  std::vector<DMat> mats;
+  std::vector<DLight> lights;
+  DCam cam;
+  int root = 0;               // root child reference (node index or encoded leaf)
+  int depth = 0;              // reference BVH depth (root = 0)
+  int ref_nodes = 0;          // node count of the reference binary tree
+  int nprim = 0;
+};
+
+// Returns BDPT_OK or an error code; err receives a message.
+int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err);
+
+}  // namespace bdpt

@@ -160,6 +160,10 @@ int bdpt_read_frame(void* ctx, int32_t which, float* rgb);
 /* Device pointer of a frame (W*H*3 float) for in-HBM consumers (RCCL reduce). */
 int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr);
 
+/* Enqueues a device-to-device copy of a frame into caller device memory (W*H*3 floats) on the
+ * ctx stream — e.g. into a torch tensor that RCCL then reduces. Async. */
+int bdpt_copy_frame(void* ctx, int32_t which, void* dst_device);
+
 int bdpt_get_stats(void* ctx, bdpt_stats* out);
 
 /* Test hook: closest-hit / any-hit queries for a batch of rays through the device BVH

@@ -119,8 +119,8 @@ inline void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1) {
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
 }
-// u = ((x >> 8) + 0.5) * 2^-24 : exact in fp32, in (0,1).
-inline float u24(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+// u = ((x >> 9) + 0.5) * 2^-23 : exact in fp32 (24 significant bits), in [2^-24, 1 - 2^-24].
+inline float u24(uint32_t x) { return ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-07f; }
 
 struct CounterStream {
   uint32_t k0, k1, pix, smp, block;
@@ -541,27 +541,33 @@ struct Tracer {
     }
     return false;
   }
-  // Sphere::test/intersect (sphere.cpp:11-35,61-93)
+  // Sphere::test/intersect (sphere.cpp:11-35,61-93). The quadratic is always solved in fp64
+  // (in mode 2 from the fp32 ray and sphere): in fp32 the reference's b*b - 4ac cancels
+  // catastrophically for rays from the camera (|o-c|^2 ~ 20 vs r^2 = 0.09), which moves hits by
+  // ~1e-5 and self-shadows the EPS_F-offset connection rays (DESIGN.md §fp32 semantics).
   bool sph_hit(const Prim<R>& S, Ray<R>& r, Isect* is, int idx) {
     st.sph++;
-    V o = r.o, d = r.d, vc = S.c;
-    R a = d.norm2();
-    R b = 2 * dot(o - vc, d);
-    R c = (o - vc).norm2() - S.r2;
-    R delta = b * b - 4 * a * c;
+    V3<double> o((double)r.o.x, (double)r.o.y, (double)r.o.z), d((double)r.d.x, (double)r.d.y, (double)r.d.z);
+    V3<double> vc((double)S.c.x, (double)S.c.y, (double)S.c.z);
+    double r2 = (sizeof(R) == 8) ? (double)S.r2 : (double)S.r * (double)S.r;
+    double a = d.norm2();
+    double b = 2 * dot(o - vc, d);
+    double c = (o - vc).norm2() - r2;
+    double delta = b * b - 4 * a * c;
     if (delta < 0) return false;
-    R root = std::sqrt(delta);
-    R t1 = (-b - root) / (2 * a);
-    R t2 = (-b + root) / (2 * a);
-    R t = -1;
-    if (t1 >= r.min_t && t1 <= r.max_t) t = t1;
-    else if (t2 >= r.min_t && t2 <= r.max_t) t = t2;
+    double root = std::sqrt(delta);
+    double t1 = (-b - root) / (2 * a);
+    double t2 = (-b + root) / (2 * a);
+    double t = -1;
+    if (t1 >= (double)r.min_t && t1 <= (double)r.max_t) t = t1;
+    else if (t2 >= (double)r.min_t && t2 <= (double)r.max_t) t = t2;
     if (t > 0) {
-      r.max_t = t;
-      V p = r.o + t * r.d;
+      R tr = (R)t;
+      r.max_t = tr;
+      V p = r.o + tr * r.d;
       V normal = p - S.c;
       normal.normalize();
-      is->t = t;
+      is->t = tr;
       is->n = normal;
       is->prim = idx;
       is->mat = S.mat;
@@ -1088,6 +1094,23 @@ struct Tracer {
     V contrib = ea * la * c;
     if (contrib.norm() > R(EPS_F)) w = mis_weight(i_eye, i_light, E, L, LS, ES);
     V ill = contrib * w;
+#ifdef ORC_DEBUG2
+    fprintf(stderr, "  (%d,%d) c=(%.6g %.6g %.6g) w=%.6g ill=(%.6g %.6g %.6g)\n", i_eye, i_light, (double)c.x,
+            (double)c.y, (double)c.z, (double)w, (double)ill.x, (double)ill.y, (double)ill.z);
+#endif
+#ifdef ORC_DEBUG
+    if (!(std::isfinite((double)ill.x))) {
+      fprintf(stderr, "NaN ill at i=%d j=%d contrib=(%g %g %g) w=%g c=(%g %g %g) ea=(%g) la=(%g)\n", i_eye, i_light,
+              (double)contrib.x, (double)contrib.y, (double)contrib.z, (double)w, (double)c.x, (double)c.y, (double)c.z,
+              (double)ea.x, (double)la.x);
+      for (size_t k = 0; k < E.size(); k++) fprintf(stderr, " E%zu pos=(%g %g %g) n=(%g %g %g) p=%g a=%g mat=%d\n", k,
+        (double)E[k].position.x, (double)E[k].position.y, (double)E[k].position.z, (double)E[k].isect.n.x,
+        (double)E[k].isect.n.y, (double)E[k].isect.n.z, (double)E[k].p, (double)E[k].alpha.x, E[k].isect.mat);
+      for (size_t k = 0; k < L.size(); k++) fprintf(stderr, " L%zu pos=(%g %g %g) n=(%g %g %g) p=%g a=%g mat=%d\n", k,
+        (double)L[k].position.x, (double)L[k].position.y, (double)L[k].position.z, (double)L[k].isect.n.x,
+        (double)L[k].isect.n.y, (double)L[k].isect.n.z, (double)L[k].p, (double)L[k].alpha.x, L[k].isect.mat);
+    }
+#endif
     if (i_eye == 1) {
       if (eye_x >= 0 && eye_y >= 0 && eye_x < W && eye_y < H) splat(eye_x, eye_y, ill / R(ns_aa));
       return V();
@@ -1105,6 +1128,14 @@ struct Tracer {
     V lrad, ln;
     Ray<R> lr = sample_light_ray(lpp, ldp, lrad, ln);
     prepare_subpath(lr, lpp, ldp, L, lrad, ln, true);
+#ifdef ORC_DEBUG2
+    for (size_t k = 0; k < E.size(); k++) fprintf(stderr, " E%zu pos=(%.8g %.8g %.8g) n=(%.6g %.6g %.6g) p=%.6g a=%.6g mat=%d\n", k,
+        (double)E[k].position.x, (double)E[k].position.y, (double)E[k].position.z, (double)E[k].isect.n.x,
+        (double)E[k].isect.n.y, (double)E[k].isect.n.z, (double)E[k].p, (double)E[k].alpha.x, E[k].isect.mat);
+    for (size_t k = 0; k < L.size(); k++) fprintf(stderr, " L%zu pos=(%.8g %.8g %.8g) n=(%.6g %.6g %.6g) p=%.6g a=%.6g mat=%d\n", k,
+        (double)L[k].position.x, (double)L[k].position.y, (double)L[k].position.z, (double)L[k].isect.n.x,
+        (double)L[k].isect.n.y, (double)L[k].isect.n.z, (double)L[k].p, (double)L[k].alpha.x, L[k].isect.mat);
+#endif
     for (int i = 1; i < (int)E.size(); i++)
       for (int j = 0; j < (int)L.size(); j++) L_out += estimate(i, j, E, L);
     return L_out;
@@ -1284,6 +1315,34 @@ int oracle_trace_rays(const bdpt_scene_desc* d, int mode, const float* rays, int
     out_t[i] = h ? (any_hit ? 0.0f : (float)is.t) : INFINITY;
     out_prim[i] = h ? (any_hit ? 0 : is.prim) : -1;
   }
+  return 0;
+}
+
+// One sample's eye-image contribution (debug / per-sample parity); splats go to light_out (W*H*3).
+int oracle_sample(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode,
+                  uint64_t seed, int x, int y, int s, double* eye_out, double* light_out) {
+  if (mode != 1 && mode != 2) return BDPT_E_INVALID;
+  std::vector<double> lb((size_t)W * H * 3, 0.0);
+  if (mode == 1) {
+    Scene<double> sc; std::string err;
+    if (load_scene<double>(d, sc, err)) return BDPT_E_INVALID;
+    CounterStream cs; cs.init(seed, (uint32_t)(x + y * W), (uint32_t)s);
+    PolicyC64 pol; pol.cs = &cs;
+    Tracer<PolicyC64> tr(sc, pol, max_depth, W, H, spp);
+    tr.light_buf = &lb;
+    V3<double> v = tr.one_sample(x, y);
+    for (int c = 0; c < 3; c++) eye_out[c] = v[c];
+  } else {
+    Scene<float> sc; std::string err;
+    if (load_scene<float>(d, sc, err)) return BDPT_E_INVALID;
+    CounterStream cs; cs.init(seed, (uint32_t)(x + y * W), (uint32_t)s);
+    PolicyC32 pol; pol.cs = &cs;
+    Tracer<PolicyC32> tr(sc, pol, max_depth, W, H, spp);
+    tr.light_buf = &lb;
+    V3<float> v = tr.one_sample(x, y);
+    for (int c = 0; c < 3; c++) eye_out[c] = v[c];
+  }
+  if (light_out) memcpy(light_out, lb.data(), lb.size() * sizeof(double));
   return 0;
 }
 
