@@ -42,7 +42,7 @@ def cpu_baseline(scene, threads: int, budget_s: float = 12.0) -> dict:
     from _util import MODE_C64, oracle_render
     done, t_tot, spp_run = 0, 0.0, 1
     s0 = 0
-    while t_tot < budget_s and spp_run <= 64:
+    while t_tot < budget_s * 0.8 and s0 < SPP:
         t0 = time.perf_counter()
         oracle_render(scene, W, H, SPP, M, MODE_C64, seed=5489, s0=s0, count=spp_run, threads=threads)
         dt = time.perf_counter() - t0
@@ -50,9 +50,7 @@ def cpu_baseline(scene, threads: int, budget_s: float = 12.0) -> dict:
         done += W * H * spp_run
         s0 += spp_run
         rate = W * H * spp_run / dt
-        spp_run = max(1, int((budget_s - t_tot) * rate / (W * H)))
-        if t_tot >= budget_s * 0.6:
-            break
+        spp_run = max(1, min(SPP - s0, int((budget_s - t_tot) * rate / (W * H))))
     return {"value": done / t_tot / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{SCENE} {W}x{H}, {done // (W * H)} spp of 128, m={M}, oracle fp64 "
                       f"(reference arithmetic) with {threads} threads, {t_tot:.1f} s"}
@@ -104,7 +102,8 @@ def main() -> int:
 
     scene = golden_scene(args.scene, W, H)
     seed = 5489
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
+    torch.cuda.set_stream(stream)
     # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
     pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index)
     pt.set_stream(stream.cuda_stream)

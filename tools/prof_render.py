@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""Minimal profiling target (no torch): renders one C2 frame (CBspheres 480x360, m=5) with N
+launches of `spp` samples through the C-ABI. Used under rocprofv3 (kernel trace / PMC passes)."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "bidirectional-pathtracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import bdpt_amd as B  # noqa: E402
+from _util import golden_scene  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "CBspheres"
+W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (480, 360)
+spp = int(sys.argv[4]) if len(sys.argv) > 4 else 128
+M = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+launches = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+sc = golden_scene(scene, W, H)
+pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489)
+t0 = time.perf_counter()
+for k in range(launches):
+    pt.raytrace_tiles([], k * spp, spp)
+pt.sync()
+dt = time.perf_counter() - t0
+print(f"{scene} {W}x{H} s{spp}x{launches} m{M}: {dt*1e3:.1f} ms, "
+      f"{W*H*spp*launches/dt/1e6:.1f} Msamples/s (incl. first-launch overhead)")
+pt.close()
