@@ -97,13 +97,14 @@ BDPT_HD f3 zaxis(f3 n) { return normalize(n); }   // make_coord_space(n).Z witho
 // ------------------------------------------------------------------------------------------------
 // Counter RNG: Philox4x32-10, counter (pixel, sample, block, 0xB1D1), key (seed lo, hi).
 struct Rng {
-  uint32_t k0, k1, pix, smp, block;
+  uint32_t k0, k1, pix, smp;
+  uint32_t pos;   // absolute uniform index: block = pos >> 2, word = pos & 3
+  uint32_t cur;   // block held in b0..b3 (0xffffffff: none)
   uint32_t b0, b1, b2, b3;
-  int idx;
 };
 BDPT_HD void rng_init(Rng& r, uint64_t seed, uint32_t pixel, uint32_t sample) {
   r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32); r.pix = pixel; r.smp = sample;
-  r.block = 0; r.idx = 4;
+  r.pos = 0; r.cur = 0xffffffffu;
 }
 BDPT_HD void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -122,15 +123,20 @@ BDPT_HD void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint
 }
 BDPT_HD float u_of(uint32_t x) { return ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-07f; }
 BDPT_HD float rng_next(Rng& r) {
-  if (r.idx == 4) {
-    r.b0 = r.pix; r.b1 = r.smp; r.b2 = r.block++; r.b3 = 0xB1D1u;
+  const uint32_t blk = r.pos >> 2;
+  if (blk != r.cur) {
+    r.b0 = r.pix; r.b1 = r.smp; r.b2 = blk; r.b3 = 0xB1D1u;
     philox(r.b0, r.b1, r.b2, r.b3, r.k0, r.k1);
-    r.idx = 0;
+    r.cur = blk;
   }
-  uint32_t x = r.idx == 0 ? r.b0 : r.idx == 1 ? r.b1 : r.idx == 2 ? r.b2 : r.b3;
-  r.idx++;
+  const uint32_t w = r.pos & 3u;
+  uint32_t x = w == 0 ? r.b0 : w == 1 ? r.b1 : w == 2 ? r.b2 : r.b3;
+  r.pos++;
   return u_of(x);
 }
+// Consume n uniforms without using them (a connection whose value is known to be zero still
+// advances the stream exactly as the reference's draws would).
+BDPT_HD void rng_skip(Rng& r, uint32_t n) { r.pos += n; }
 
 // cos/sin(2*pi*u), u in (0,1): quadrant split + Taylor polynomials (same as the oracle's).
 BDPT_HD void cos_sin_2pi(float u, float* c, float* s) {
@@ -205,6 +211,13 @@ struct Hit {
   float b1, b2;
 };
 
+BDPT_HD bool quot_neg(float n, float d) {
+  return ((n < 0 && d > 0) || (n > 0 && d < 0)) && fabsf(n) >= fabsf(d) * 8.67361738e-19f;  // 2^-60
+}
+BDPT_HD bool quot_gt1(float n, float d) {
+  return ((n > 0 && d > 0) || (n < 0 && d < 0)) && fabsf(n) > fabsf(d);
+}
+
 // Möller–Trumbore exactly as Triangle::intersect (triangle.cpp:57-95), fp32.
 BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f3 d, float tmin, float tmax,
                       float* t_out, float* b1_out, float* b2_out) {
@@ -212,17 +225,35 @@ BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f
   f3 e1 = mk3(g0.w, g1.x, g1.y);
   f3 e2 = mk3(g1.z, g1.w, g2.x);
   f3 s = sub(o, p0);
-  f3 s1 = cross(d, e2), s2 = cross(s, e1);
+  f3 s1 = cross(d, e2);
   float denom = dot(s1, e1);
-  float t = dot(s2, e2) / denom;
-  float b1 = dot(s1, s) / denom;
-  float b2 = dot(s2, d) / denom;
+  float n1 = dot(s1, s);
+  // Exact early-outs before the three correctly-rounded divisions: only when the rounded
+  // quotient is certainly < 0 (opposite signs, |q| >= 2^-60 so it cannot round to -0) or > 1
+  // (|n| > |denom| implies fl(n/denom) > 1), i.e. exactly when the reference test fails anyway.
+  if (quot_neg(n1, denom) || quot_gt1(n1, denom)) return false;
+  f3 s2 = cross(s, e1);
+  float n2 = dot(s2, d);
+  if (quot_neg(n2, denom) || quot_gt1(n2, denom)) return false;
+  float nt = dot(s2, e2);
+  if (tmin >= 0 && quot_neg(nt, denom)) return false;
+  float t = nt / denom;
+  float b1 = n1 / denom;
+  float b2 = n2 / denom;
   *t_out = t; *b1_out = b1; *b2_out = b2;
   return t >= tmin && t <= tmax && b1 >= 0 && b2 >= 0 && b1 + b2 <= 1;
 }
 
 // Sphere::test + intersect (sphere.cpp:11-35,61-93) with the quadratic in fp64.
 BDPT_HD bool sph_test(const float4 g0, f3 o, f3 d, float tmin, float tmax, float* t_out) {
+  {
+    // Conservative fp32 miss test: squared distance of the centre from the ray's line exceeds r^2
+    // by far more than the fp32 error (~1e-6 |o-c|^2), so the fp64 discriminant is < 0 too.
+    f3 f = sub(o, mk3(g0.x, g0.y, g0.z));
+    float a = norm2(d), bh = dot(f, d), ff = norm2(f);
+    float dl2a = ff * a - bh * bh;   // a * dist^2(centre, line)
+    if (dl2a > a * (g0.w * g0.w * 1.001f + ff * 1e-5f)) return false;
+  }
   double ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
   double cx = g0.x, cy = g0.y, cz = g0.z, r = g0.w;
   double r2 = r * r;
@@ -518,6 +549,7 @@ BDPT_HD float pdf_b(const DMat& M, f3 n, f3 zh, f3 dw) {
 
 // ------------------------------------------------------------------------------------------------
 // Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
+// Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
 struct Vtx {
   f3 pos, n, zh, alpha;
   float woz;   // eye: (w2o*normalize(E[k-1]-E[k])).z ; light: same with L[k-1]  (f() hemisphere test)
@@ -537,6 +569,7 @@ struct Paths {
   Vtx E[MAXV];       // E[k] at index k-2 (k >= 2): eye hits
   Vtx L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
+  uint32_t dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
   float l1_dir_pdf;
 };
 
@@ -545,14 +578,17 @@ struct SampleParams {
   uint64_t seed;
 };
 
-// Subpath random walk (prepare_bidirectional_subpath, bidirection.cpp:20-102).
+// Subpath random walk (prepare_bidirectional_subpath, bidirection.cpp:20-102). Vertex k of the
+// reference path is written to out[k - 2]; bit k of *dmask marks delta BSDFs.
 template <int MAXV>
 BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, float tmin, float tmax,
-                        float point_pdf, float dir_pdf, f3 init_rad, f3 init_n, int max_depth, Vtx* out) {
+                        float point_pdf, float dir_pdf, f3 init_rad, f3 init_n, int max_depth, Vtx* out,
+                        uint32_t* dmask) {
   f3 prev_alpha = divs(init_rad, point_pdf);
   float prev_pdf = dir_pdf;
   f3 prev_f = splat3(1.0f), prev_n = init_n;
   int i = 2, count = 0;
+  uint32_t dm = 0;
   f3 ro = o, rd = d;
   float rmin = tmin, rmax = tmax;
   for (;;) {
@@ -578,6 +614,7 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
     v.mat = mat;
     v.woz = 0; v.fwd = 1; v.q = 0; v.revg = 0;
     out[count++] = v;
+    if (is_delta(M.type)) dm |= 1u << i;
     if (i >= max_depth + 1 || count >= MAXV) break;
     ro = hit_p; rd = wi_world; rmin = BDPT_EPS_F; rmax = INFINITY;
     prev_f = fv;
@@ -586,6 +623,7 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
     prev_alpha = v.alpha;
     i++;
   }
+  *dmask = dm;
   return count;
 }
 
@@ -759,33 +797,30 @@ BDPT_HD EyeSample camera_sample(const DCam& c, int W, int H, f3 p) {
 BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
 
 // multiple_importance_sampling_weight (bidirection.cpp:121-293) with cached path constants.
-// i, j: reference vertex indices; vs: connection endpoint on the light side for the eye walk
-// (LS for j == 1, L[j] otherwise); es: camera sample for i == 1.
+// i, j: reference vertex indices; ls: fresh light sample (j == 1); es: camera sample (i == 1);
+// dc, dist: normalize(vl - ve) and |vl - ve| of the connection (j >= 1), which are exactly the
+// endpoint-step directions the reference recomputes (normalize(-v) == -normalize(v) in IEEE).
 template <int MAXV>
 BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j, const LightSample& ls,
-                         const EyeSample& es, int eye_light) {
+                         const EyeSample& es, int eye_light, f3 dc, float dist) {
   float w_inv = 0.0f, ratio = 1.0f;
   w_inv += ratio;
   if (i >= 2) {
     const Vtx& cur = P.E[i - 2];
     float nom;
     if (j == 0) {
-      float p = 1.0f / S.lights[eye_light].area;
-      if (S.lights[eye_light].type == LIGHT_POINT) p = 1.0f;
+      float p = S.lights[eye_light].type == LIGHT_POINT ? 1.0f : 1.0f / S.lights[eye_light].area;
       nom = p * 1.0f;
     } else {
-      f3 ppos = j == 1 ? ls.pos : P.L[j - 1].pos;
       f3 pzh = j == 1 ? ls.zh : P.L[j - 1].zh;
-      f3 dw;
-      float g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+      f3 dw = neg(dc);   // normalize(E[i] - vl)
+      float g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
       float p = j == 1 ? ls.dir_pdf * 1.0f
                        : pdf_b(S.mats[P.L[j - 1].mat], P.L[j - 1].n, pzh, dw) * 1.0f;
       nom = p * g;
     }
     ratio *= nom / cur.fwd;
-    int prev_mat = i == 2 ? -1 : P.E[i - 3].mat;
-    bool dl = is_delta(S.mats[cur.mat].type) || (prev_mat >= 0 && is_delta(S.mats[prev_mat].type));
-    if (!dl) w_inv += ratio * ratio;
+    if (!((P.dE >> (i - 1)) & 3u)) w_inv += ratio * ratio;       // delta(E[i]) || delta(E[i-1])
     for (int k = i - 1; k >= 2; k--) {
       const Vtx& v = P.E[k - 2];
       float q;
@@ -797,44 +832,40 @@ BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j,
         q = v.q;
       }
       ratio *= q;
-      int pm = k == 2 ? -1 : P.E[k - 3].mat;
-      bool d2 = is_delta(S.mats[v.mat].type) || (pm >= 0 && is_delta(S.mats[pm].type));
-      if (!d2) w_inv += ratio * ratio;
+      if (!((P.dE >> (k - 1)) & 3u)) w_inv += ratio * ratio;
     }
   }
   ratio = 1.0f;
   if (j >= 1) {
     const Vtx& cur = P.L[j - 1];
-    f3 ppos = i == 1 ? es.pos : P.E[i - 2].pos;
     f3 pzh = i == 1 ? es.zh : P.E[i - 2].zh;
     f3 dw;
-    float g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+    float g;
+    if (j >= 2) {   // cur = L[j] = vl: normalize(L[j] - ve) = dc
+      dw = dc;
+      g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
+    } else {        // cur = the original L[1], not the fresh sample (quirk 5)
+      f3 ppos = i == 1 ? es.pos : P.E[i - 2].pos;
+      g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+    }
     float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[P.E[i - 2].mat], P.E[i - 2].n, pzh, dw) * 1.0f;
     float nom = p * g;
     ratio *= nom / cur.fwd;
-    int prev_mat = j == 1 ? -1 : P.L[j - 2].mat;
-    bool dl = (cur.mat >= 0 && is_delta(S.mats[cur.mat].type)) || (prev_mat >= 0 && is_delta(S.mats[prev_mat].type));
-    if (!dl) w_inv += ratio * ratio;
+    if (!((P.dL >> (j - 1)) & 3u)) w_inv += ratio * ratio;
     for (int k = j - 1; k >= 1; k--) {
-      const Vtx& v = P.L[k - 1];
-      ratio *= v.q;
-      int pm = k == 1 ? -1 : P.L[k - 2].mat;
-      bool d2 = (v.mat >= 0 && is_delta(S.mats[v.mat].type)) || (pm >= 0 && is_delta(S.mats[pm].type));
-      if (!d2) w_inv += ratio * ratio;
+      ratio *= P.L[k - 1].q;
+      if (!((P.dL >> (k - 1)) & 3u)) w_inv += ratio * ratio;
     }
   }
   return 1.0f / w_inv;
 }
 
-// One pixel-sample: est_radiance_global_illumination (bidirection.cpp:472-500) with the
-// connection loop estimate_bidirection_radiance (:296-469). Returns the eye-image value;
-// light-image splats (t = 1) go to sink.splat(x, y, value / spp).
-template <int MAXV, class Sink>
-BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt,
-                         int x, int y, uint32_t sample, Sink& sink) {
-  Rng g;
+// Eye and light subpaths of one pixel-sample plus their MIS constants
+// (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524).
+template <int MAXV>
+BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
+                            int x, int y, uint32_t sample) {
   rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
-  // raytrace_pixel (bidirection.cpp:515-524)
   float px, py;
   grid2d(g, &px, &py);
   px = px + (float)x;
@@ -842,11 +873,10 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
   float dx = px / (float)sp.W, dy = py / (float)sp.H;
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   f3 rd = camera_dir(S.cam, dx, dy);
-  // eye subpath
   int ne = random_walk<MAXV>(S, g, cnt, cam, rd, S.cam.nclip, S.cam.fclip, 1.0f, 1.0f, splat3(1.0f), rd,
-                             sp.max_depth, P.E);
+                             sp.max_depth, P.E, &P.dE);
   P.nE = ne + 2;
-  // light subpath (sample_light_ray, bidirection.cpp:105-118)
+  // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le
   int lid = (int)(rng_next(g) * (float)S.nlights);
   if (lid >= S.nlights) lid = S.nlights - 1;
   const DLight& L0 = S.lights[lid];
@@ -891,96 +921,156 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
     v1.q = 0; v1.revg = 0; v1.woz = 0;
   }
   P.l1_dir_pdf = ldp;
-  int nl = random_walk<MAXV>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1);
+  uint32_t dl = 0;
+  int nl = random_walk<MAXV>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1, &dl);
+  P.dL = dl;
   P.nL = nl + 2;
   eye_constants<MAXV>(S, P);
   light_constants<MAXV>(S, P, lpp);
+}
 
-  const float inv_spp = 1.0f / (float)sp.spp;
+// What estimate_bidirection_radiance (bidirection.cpp:296-469) computes for pair (i, j) up to its
+// visibility test: either nothing (zero contribution), a direct eye-image value (s = 0, no ray),
+// or a connection ray on [EPS_F, tmax] whose value (MIS-weighted) counts if it is unoccluded.
+enum { CONN_NONE = 0, CONN_DIRECT = 1, CONN_RAY = 2 };
+struct Conn {
+  f3 o, d;
+  float tmax;
+  f3 val;      // eye image: ill; light image: ill / ns_aa
+  int splat;   // -1: eye image of this sample's pixel; else x + y*W of the t = 1 splat
+};
+
+// A vertex that can receive a connection: diffuse (f != 0 only for DiffuseBSDF, bsdf.cpp:52-62),
+// viewed from its front side (wo.z >= 0) and carrying throughput.
+BDPT_HD bool can_connect(const SceneView& S, const Vtx& v) {
+  return S.mats[v.mat].type == MAT_DIFFUSE && v.woz >= 0 && nonzero3(v.alpha);
+}
+// Uniforms consumed by the fresh light sample of a j == 1 connection (rand_light + sample_Le_point).
+BDPT_HD void skip_light_sample(const SceneView& S, Rng& g) {
+  if (S.nlights == 1) {
+    rng_skip(g, S.lights[0].type == LIGHT_POINT ? 1u : 3u);
+    return;
+  }
+  int id = (int)(rng_next(g) * (float)S.nlights);
+  if (id >= S.nlights) id = S.nlights - 1;
+  if (S.lights[id].type != LIGHT_POINT) rng_skip(g, 2);
+}
+
+template <int MAXV>
+BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const Paths<MAXV>& P, Rng& g, int i, int j,
+                      Conn& cn) {
+  const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
+  const bool eye_cam = i == 1;
+  const Vtx* ev = eye_cam ? nullptr : &P.E[i - 2];
+  LightSample ls;
+  EyeSample es;
+  es.x = -1; es.y = -1;
+  cn.splat = -1;
+  if (j == 0) {
+    if (eye_cam) return CONN_NONE;
+    const DMat& M = S.mats[ev->mat];
+    if (M.type != MAT_EMISSION) return CONN_NONE;
+    f3 c = mk3(M.a[0], M.a[1], M.a[2]);
+    if (!(norm(c) > BDPT_EPS_F)) return CONN_NONE;
+    int eye_light = -1;
+    for (int l = 0; l < S.nlights; l++)
+      if (light_contains(S.lights[l], ev->pos)) { eye_light = l; break; }
+    if (eye_light < 0) return CONN_NONE;
+    f3 prevp = i == 2 ? cam : P.E[i - 3].pos;
+    f3 wi = normalize(sub(ev->pos, prevp));
+    const DLight& EL = S.lights[eye_light];
+    if (!(light_dir_pdf(EL, wi) > 0)) return CONN_NONE;
+    c = mk3(EL.rad[0], EL.rad[1], EL.rad[2]);
+    f3 contrib = mul(mul(ev->alpha, splat3(1.0f)), c);
+    float w = 0;
+    if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, 0, ls, es, eye_light, splat3(0), 0);
+    cn.val = muls(contrib, w);
+    return CONN_DIRECT;
+  }
+  // Zero-contribution connections (f_eye = 0 or f_light = 0 or zero throughput) end here; only
+  // the RNG draws of a fresh light sample (j == 1) must still happen.
+  if (!eye_cam && !can_connect(S, *ev)) {
+    if (j == 1) skip_light_sample(S, g);
+    return CONN_NONE;
+  }
+  if (j >= 2 && !can_connect(S, P.L[j - 1])) return CONN_NONE;
+  f3 vl_pos, vl_n, la;
+  if (j == 1) {   // fresh light sample (bidirection.cpp:332-358)
+    const f3 epos = eye_cam ? cam : ev->pos;
+    int id = (int)(rng_next(g) * (float)S.nlights);
+    if (id >= S.nlights) id = S.nlights - 1;
+    float lp;
+    ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
+    vl_pos = ls.pos; vl_n = ls.n; la = ls.alpha;
+  } else {
+    const Vtx& lv = P.L[j - 1];
+    vl_pos = lv.pos; vl_n = lv.n; la = lv.alpha;
+  }
+  f3 ve_pos, ve_n, ea;
+  if (eye_cam) {   // camera sample (bidirection.cpp:360-383)
+    es = camera_sample(S.cam, sp.W, sp.H, vl_pos);
+    if (!(es.x >= 0 && es.y >= 0 && es.x < sp.W && es.y < sp.H)) return CONN_NONE;   // not splatted
+    ve_pos = es.pos; ve_n = es.n; ea = es.alpha;
+  } else {
+    ve_pos = ev->pos; ve_n = ev->n; ea = ev->alpha;
+  }
+  f3 eal = mul(ea, la);
+  if (!nonzero3(eal)) return CONN_NONE;
+  // One direction serves the f() hemisphere tests, the connection ray and both MIS endpoint steps.
+  f3 dc = sub(vl_pos, ve_pos);
+  float dist = norm(dc);
+  dc = normalize(dc);
+  f3 f_eye = splat3(1.0f), f_light = splat3(1.0f);
+  if (!eye_cam) {
+    if (lz(dc, ev->zh) < 0) return CONN_NONE;   // f_eye = 0 (bsdf.cpp:56-58)
+    const DMat& M = S.mats[ev->mat];
+    f_eye = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
+  }
+  if (j >= 2) {
+    const Vtx& lv = P.L[j - 1];
+    if (lz(neg(dc), lv.zh) < 0) return CONN_NONE;   // f_light = 0
+    const DMat& M = S.mats[lv.mat];
+    f_light = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
+  }
+  float gg = fabsf(dot(vl_n, dc) * dot(ve_n, dc)) / (dist * dist);
+  f3 c = mul(muls(f_eye, gg), f_light);
+  f3 contrib = mul(eal, c);
+  if (!(norm(contrib) > BDPT_EPS_F)) return CONN_NONE;   // w = 0
+  float w = mis_weight<MAXV>(S, P, i, j, ls, es, -1, dc, dist);
+  f3 ill = muls(contrib, w);
+  cn.o = ve_pos;
+  cn.d = dc;
+  cn.tmax = dist - BDPT_EPS_F;
+  if (eye_cam) {
+    cn.val = divs(ill, (float)sp.spp);
+    cn.splat = es.x + es.y * sp.W;
+  } else {
+    cn.val = ill;
+  }
+  return CONN_RAY;
+}
+
+// One pixel-sample, connections resolved in the reference's (i, j) order (host/test use; the
+// device kernel defers the connection rays to a wave-compacted queue instead).
+template <int MAXV, class Sink>
+BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt,
+                         int x, int y, uint32_t sample, Sink& sink) {
+  Rng g;
+  prepare_sample<MAXV>(S, sp, P, cnt, g, x, y, sample);
   f3 eye_sum = splat3(0);
   for (int i = 1; i < P.nE; i++) {
-    const bool eye_cam = i == 1;
-    const Vtx* ev = eye_cam ? nullptr : &P.E[i - 2];
-    const f3 epos = eye_cam ? cam : ev->pos;
     for (int j = 0; j < P.nL; j++) {
-      LightSample ls;
-      EyeSample es;
-      es.x = -1; es.y = -1;
-      f3 c = splat3(0);
-      int eye_light = -1;
-      if (j == 0) {
-        if (eye_cam) continue;
-        const DMat& M = S.mats[ev->mat];
-        if (M.type != MAT_EMISSION) continue;
-        c = mk3(M.a[0], M.a[1], M.a[2]);
-        if (!(norm(c) > BDPT_EPS_F)) continue;
-        for (int l = 0; l < S.nlights; l++)
-          if (light_contains(S.lights[l], ev->pos)) { eye_light = l; break; }
-        if (eye_light < 0) continue;
-        f3 prevp = i == 2 ? cam : P.E[i - 3].pos;
-        f3 wi = normalize(sub(ev->pos, prevp));
-        const DLight& EL = S.lights[eye_light];
-        if (!(light_dir_pdf(EL, wi) > 0)) continue;
-        c = mk3(EL.rad[0], EL.rad[1], EL.rad[2]);
-        f3 contrib = mul(mul(ev->alpha, splat3(1.0f)), c);
-        float w = 0;
-        if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, 0, ls, es, eye_light);
-        eye_sum = add(eye_sum, muls(contrib, w));
-        continue;
-      }
-      // f_light / vl
-      f3 vl_pos, vl_n, la;
-      if (j == 1) {
-        int id = (int)(rng_next(g) * (float)S.nlights);
-        if (id >= S.nlights) id = S.nlights - 1;
-        float lp;
-        ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
-        vl_pos = ls.pos; vl_n = ls.n; la = ls.alpha;
-      } else {
-        const Vtx& lv = P.L[j - 1];
-        vl_pos = lv.pos; vl_n = lv.n; la = lv.alpha;
-      }
-      f3 ve_pos, ve_n, ea;
-      if (eye_cam) {
-        es = camera_sample(S.cam, sp.W, sp.H, vl_pos);
-        ve_pos = es.pos; ve_n = es.n; ea = es.alpha;
-      } else {
-        ve_pos = ev->pos; ve_n = ev->n; ea = ev->alpha;
-      }
-      f3 f_eye = splat3(1.0f), f_light = splat3(1.0f);
-      if (!eye_cam) {
-        const DMat& M = S.mats[ev->mat];
-        float cz = lz(normalize(sub(vl_pos, ev->pos)), ev->zh);
-        if (M.type != MAT_DIFFUSE || ev->woz < 0 || cz < 0) continue;   // f_eye = 0
-        f_eye = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
-      }
-      if (j >= 2) {
-        const Vtx& lv = P.L[j - 1];
-        const DMat& M = S.mats[lv.mat];
-        float cz = lz(normalize(sub(ve_pos, lv.pos)), lv.zh);
-        if (M.type != MAT_DIFFUSE || cz < 0 || lv.woz < 0) continue;   // f_light = 0
-        f_light = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
-      }
-      f3 eal = mul(ea, la);
-      if (!nonzero3(eal)) continue;
-      f3 conn = sub(vl_pos, ve_pos);
-      float dist = norm(conn);
-      conn = normalize(conn);
-      if (trace_any(S, ve_pos, conn, BDPT_EPS_F, dist - BDPT_EPS_F, cnt)) continue;
-      float gg = fabsf(dot(vl_n, conn) * dot(ve_n, conn)) / (dist * dist);
-      c = mul(muls(f_eye, gg), f_light);
-      f3 contrib = mul(eal, c);
-      float w = 0;
-      if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, j, ls, es, -1);
-      f3 ill = muls(contrib, w);
-      if (eye_cam) {
-        if (es.x >= 0 && es.y >= 0 && es.x < sp.W && es.y < sp.H) sink.splat(es.x, es.y, divs(ill, (float)sp.spp));
-      } else {
-        eye_sum = add(eye_sum, ill);
+      Conn cn;
+      int kind = make_conn<MAXV>(S, sp, P, g, i, j, cn);
+      if (kind == CONN_DIRECT) {
+        eye_sum = add(eye_sum, cn.val);
+      } else if (kind == CONN_RAY) {
+        if (trace_any(S, cn.o, cn.d, BDPT_EPS_F, cn.tmax, cnt)) continue;
+        if (cn.splat >= 0) sink.splat(cn.splat % sp.W, cn.splat / sp.W, cn.val);
+        else eye_sum = add(eye_sum, cn.val);
       }
     }
   }
-  (void)inv_spp;
   return eye_sum;
 }
 

@@ -33,6 +33,7 @@ struct KParams {
   float* eye;        // W*H*3
   float* light;      // W*H*3
   unsigned long long* stats;  // 8 counters
+  unsigned long long* prof;   // phase cycle counters (BDPT_PHASE_PROF builds only)
   const int4* blocks;         // tile blocks (x0, y0, w, h) of <= 8x8 pixels; null = full frame
   int nblocks;
   int nbx;                    // full-frame: blocks per row
@@ -41,32 +42,79 @@ struct KParams {
   long long nlanes;
 };
 
-struct DevSink {
-  float* light;
-  int W;
-  __device__ void splat(int x, int y, f3 v) {
-    float* p = light + 3 * ((size_t)x + (size_t)y * W);
-    atomicAdd(p, v.x);
-    atomicAdd(p + 1, v.y);
-    atomicAdd(p + 2, v.z);
-  }
-};
-
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// number of set bits of m below this lane (ballot + mbcnt prefix sum)
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
 
+// Wave-local ring of deferred connection rays in LDS (SoA, 128 slots per wave).
+constexpr int QCAP = 128;
+struct WaveQ {
+  float ox[QCAP], oy[QCAP], oz[QCAP], dx[QCAP], dy[QCAP], dz[QCAP], tmax[QCAP];
+  float vx[QCAP], vy[QCAP], vz[QCAP];
+  int tgt[QCAP];            // >= 0: light-image pixel (t = 1 splat); < 0: ~owner lane (eye image)
+  float acc[3][64];         // eye-image accumulators of the wave's 64 lanes
+};
+
+// Resolve n (<= 64) queued connection rays, one per lane: any-hit test, then add the value of the
+// unoccluded ones to the owner's eye accumulator (LDS atomic) or splat it (global atomic).
+__device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int head, int n, int lane, float* light,
+                                            Counters& cnt) {
+  if (lane < n) {
+    const int k = (head + lane) & (QCAP - 1);
+    f3 o = mk3(q.ox[k], q.oy[k], q.oz[k]), d = mk3(q.dx[k], q.dy[k], q.dz[k]);
+    const float tmax = q.tmax[k], vx = q.vx[k], vy = q.vy[k], vz = q.vz[k];
+    const int tgt = q.tgt[k];
+    if (!trace_any(S, o, d, BDPT_EPS_F, tmax, cnt)) {
+      if (tgt < 0) {
+        const int ow = ~tgt;
+        atomicAdd(&q.acc[0][ow], vx);
+        atomicAdd(&q.acc[1][ow], vy);
+        atomicAdd(&q.acc[2][ow], vz);
+      } else {
+        float* p = light + 3 * (size_t)tgt;
+        atomicAdd(p, vx);
+        atomicAdd(p + 1, vy);
+        atomicAdd(p + 2, vz);
+      }
+    }
+  }
+}
+
+// k_bdpt_sample: each lane owns one pixel and a chunk of its samples. Per sample the lane builds
+// both subpaths (random walks, closest-hit traversal) and then enumerates its (i, j) connections
+// in the reference's order; every connection that needs a visibility ray is pushed (ballot +
+// mbcnt compaction) into the wave's LDS ring, and whenever 64 are queued the whole wave traces
+// them together — all 64 lanes busy on shadow rays regardless of per-lane path lengths.
 template <int MAXV, bool STATS>
-__global__ __launch_bounds__(128) void k_bdpt_sample(KParams kp) {
-  const long long lane = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+#ifndef BDPT_MIN_WAVES
+#define BDPT_MIN_WAVES 4   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
+#endif
+__global__ __launch_bounds__(128, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
+  __shared__ WaveQ qs[2];
+  const int lane = threadIdx.x & 63;
+  WaveQ& q = qs[threadIdx.x >> 6];
+  const long long gl = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   Counters cnt = {0, 0, 0, 0, 0, 0};
   unsigned nsamp = 0;
-  if (lane < kp.nlanes) {
-    const long long chunk = lane / kp.lanes_per_chunk;
-    const long long within = lane - chunk * kp.lanes_per_chunk;
-    const int blk = (int)(within >> 6), q = (int)(within & 63);
+  q.acc[0][lane] = 0;
+  q.acc[1][lane] = 0;
+  q.acc[2][lane] = 0;
+  int x = 0, y = 0, s0 = 0, s1 = 0;
+  if (gl < kp.nlanes) {
+    const long long chunk = gl / kp.lanes_per_chunk;
+    const long long within = gl - chunk * kp.lanes_per_chunk;
+    const int blk = (int)(within >> 6), qq = (int)(within & 63);
     int bx0, by0, bw, bh;
     if (kp.blocks) {
       int4 b = kp.blocks[blk];
@@ -77,34 +125,115 @@ __global__ __launch_bounds__(128) void k_bdpt_sample(KParams kp) {
       bw = min(8, kp.sp.W - bx0);
       bh = min(8, kp.sp.H - by0);
     }
-    const int qx = q & 7, qy = q >> 3;
+    const int qx = qq & 7, qy = qq >> 3;
     if (qx < bw && qy < bh) {
-      const int x = bx0 + qx, y = by0 + qy;
-      const int s0 = kp.spp_begin + (int)chunk * kp.spl;
-      const int s1 = min(s0 + kp.spl, kp.spp_end);
-      Paths<MAXV> P;
-      DevSink sink{kp.light, kp.sp.W};
-      const float inv = 1.0f / (float)kp.sp.spp;
-      float ax = 0, ay = 0, az = 0;
-      for (int s = s0; s < s1; s++) {
-        f3 v = render_sample<MAXV>(kp.S, kp.sp, P, cnt, x, y, (uint32_t)s, sink);
-        ax += v.x * inv;
-        ay += v.y * inv;
-        az += v.z * inv;
-        nsamp++;
-      }
-      float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
-      if (ax != 0) atomicAdd(e, ax);
-      if (ay != 0) atomicAdd(e + 1, ay);
-      if (az != 0) atomicAdd(e + 2, az);
+      x = bx0 + qx;
+      y = by0 + qy;
+      s0 = kp.spp_begin + (int)chunk * kp.spl;
+      s1 = min(s0 + kp.spl, kp.spp_end);
     }
   }
+  const int my_n = max(0, s1 - s0);
+  const int wave_n = wave_max(my_n);
+  const float inv = 1.0f / (float)kp.sp.spp;
+  float dxs = 0, dys = 0, dzs = 0;   // direct (s = 0) eye contributions
+  int head = 0, tail = 0;            // wave-uniform ring indices
+  Paths<MAXV> P;
+#ifdef BDPT_PHASE_PROF
+  unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
+#define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define PH_STAMP(v)
+#endif
+  for (int t = 0; t < wave_n; t++) {
+    Rng g;
+    int nE = 0, nL = 0;
+    PH_STAMP(tp0);
+    if (t < my_n) {
+      prepare_sample<MAXV>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
+      nE = P.nE;
+      nL = P.nL;
+      nsamp++;
+    }
+    // wave-uniform (i, j) loops: every lane is at the same strategy at the same time, so the
+    // j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
+    // for all lanes instead of interleaving with the general case.
+    const int wE = wave_max(nE), wL = wave_max(nL);
+    PH_STAMP(tp1);
+#ifdef BDPT_PHASE_PROF
+    ph_prep += tp1 - tp0;
+    unsigned long long tg0 = tp1;
+#endif
+    for (int i = 1; i < wE; i++)
+    for (int j = 0; j < wL; j++) {
+      int kind = CONN_NONE;
+      Conn cn;
+      if (i < nE && j < nL) {
+        kind = make_conn<MAXV>(kp.S, kp.sp, P, g, i, j, cn);
+        if (kind == CONN_DIRECT) {
+          dxs += cn.val.x * inv;
+          dys += cn.val.y * inv;
+          dzs += cn.val.z * inv;
+        }
+      }
+      const bool push = kind == CONN_RAY;
+      const unsigned long long m = __ballot(push);
+      if (push) {
+        const int slot = (tail + lanes_below(m)) & (QCAP - 1);
+        q.ox[slot] = cn.o.x; q.oy[slot] = cn.o.y; q.oz[slot] = cn.o.z;
+        q.dx[slot] = cn.d.x; q.dy[slot] = cn.d.y; q.dz[slot] = cn.d.z;
+        q.tmax[slot] = cn.tmax;
+        const bool eye_t = cn.splat < 0;
+        q.vx[slot] = eye_t ? cn.val.x * inv : cn.val.x;
+        q.vy[slot] = eye_t ? cn.val.y * inv : cn.val.y;
+        q.vz[slot] = eye_t ? cn.val.z * inv : cn.val.z;
+        q.tgt[slot] = eye_t ? ~lane : cn.splat;
+      }
+      tail += __popcll(m);
+      if (tail - head >= 64) {
+        PH_STAMP(tp0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        flush_queue(kp.S, q, head, 64, lane, kp.light, cnt);
+        __builtin_amdgcn_wave_barrier();
+        head += 64;
+        PH_STAMP(tp1);
+#ifdef BDPT_PHASE_PROF
+        ph_flush += tp1 - tp0;
+#endif
+      }
+    }
+#ifdef BDPT_PHASE_PROF
+    ph_gen += __builtin_amdgcn_s_memtime() - tg0;
+#endif
+  }
+  if (tail > head) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    flush_queue(kp.S, q, head, tail - head, lane, kp.light, cnt);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (my_n > 0) {
+    float ax = q.acc[0][lane] + dxs, ay = q.acc[1][lane] + dys, az = q.acc[2][lane] + dzs;
+    float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
+    if (ax != 0) atomicAdd(e, ax);
+    if (ay != 0) atomicAdd(e + 1, ay);
+    if (az != 0) atomicAdd(e + 2, az);
+  }
+#ifdef BDPT_PHASE_PROF
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
+    atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
+    atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
+  }
+#endif
   if (STATS) {
     unsigned v[7] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits};
 #pragma unroll
     for (int k = 0; k < 7; k++) {
       unsigned s = wave_sum(v[k]);
-      if ((threadIdx.x & 63) == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
+      if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
     }
   }
 }
@@ -253,7 +382,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   size_t fb = c->npix * 3 * sizeof(float);
   if (hipMalloc((void**)&c->d_eye, fb) != hipSuccess || hipMalloc((void**)&c->d_light, fb) != hipSuccess ||
       hipMalloc((void**)&c->d_sample, fb) != hipSuccess ||
-      hipMalloc((void**)&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "out of device memory";
     return fail(BDPT_E_NOMEM);
   }
@@ -265,7 +394,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->stream = c->own;
   if (hipMemsetAsync(c->d_eye, 0, fb, c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_light, 0, fb, c->stream) != hipSuccess ||
-      hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess) { g_err = "init sync failed"; return fail(BDPT_E_DEVICE); }
   *ctx_out = c;
   return BDPT_OK;
@@ -293,7 +422,7 @@ int bdpt_clear(void* ctx) {
   size_t fb = c->npix * 3 * sizeof(float);
   HIPCHK(hipMemsetAsync(c->d_eye, 0, fb, c->stream));
   HIPCHK(hipMemsetAsync(c->d_light, 0, fb, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream));
   return BDPT_OK;
 }
 
@@ -310,6 +439,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.eye = c->d_eye;
   kp.light = c->d_light;
   kp.stats = c->d_stats;
+  kp.prof = c->d_stats + 8;
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);
@@ -428,6 +558,15 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   out->last_kernel_ms = ms;
   out->bvh_nodes = (uint64_t)c->hs.ref_nodes;
   out->bvh_depth = (uint64_t)c->hs.depth;
+  return BDPT_OK;
+}
+
+int bdpt_debug_counters(void* ctx, uint64_t* out16) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !out16) { g_err = "null argument"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out16, c->d_stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return BDPT_OK;
 }
 

@@ -172,6 +172,10 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out);
 int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, float* out_t,
                     int32_t* out_prim);
 
+/* Diagnostic hook: raw device counters (8 stats words + 8 phase-cycle words of a
+ * BDPT_PHASE_PROF build). Sync. */
+int bdpt_debug_counters(void* ctx, uint64_t* out16);
+
 #ifdef __cplusplus
 }
 #endif

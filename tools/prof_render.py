@@ -16,13 +16,28 @@ W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (480, 360)
 spp = int(sys.argv[4]) if len(sys.argv) > 4 else 128
 M = int(sys.argv[5]) if len(sys.argv) > 5 else 5
 launches = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+if os.environ.get("BDPT_LIB"):
+    B.load_library(os.environ["BDPT_LIB"])
+    B._lib = B.load_library(os.environ["BDPT_LIB"])
 sc = golden_scene(scene, W, H)
 pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489)
+if os.environ.get("BDPT_WARM", "1") == "1":   # code-object load + first-launch setup, untimed
+    pt.raytrace_tiles([], 0, 1)
+    pt.sync()
+    pt.clear()
 t0 = time.perf_counter()
 for k in range(launches):
     pt.raytrace_tiles([], k * spp, spp)
 pt.sync()
 dt = time.perf_counter() - t0
 print(f"{scene} {W}x{H} s{spp}x{launches} m{M}: {dt*1e3:.1f} ms, "
-      f"{W*H*spp*launches/dt/1e6:.1f} Msamples/s (incl. first-launch overhead)")
+      f"{W*H*spp*launches/dt/1e6:.1f} Msamples/s ")
+if os.environ.get("BDPT_PHASES"):
+    import ctypes as C
+    arr = (C.c_uint64 * 16)()
+    pt.lib.bdpt_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    pt.lib.bdpt_debug_counters(pt.ctx, arr)
+    tot = arr[8] + arr[9] + arr[10]
+    print("phase cycles (wave-summed): prepare %.3g (%.1f%%)  conn-gen %.3g (%.1f%%)  flush %.3g (%.1f%%)" % (
+        arr[8], 100 * arr[8] / tot, arr[9], 100 * arr[9] / tot, arr[10], 100 * arr[10] / tot))
 pt.close()
