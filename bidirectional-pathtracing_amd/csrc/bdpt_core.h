@@ -196,6 +196,9 @@ struct SceneView {
   const DLight* lights;
   int nlights;
   int root;              // root child reference
+  const float4* lnodes;  // LDS copy of nodes [0, ntop) (LM 1: all nodes; LM 2: BFS treelet)
+  const float4* lgeom;   // LDS copy of the geometry (LM 1 only)
+  int ntop;
   DCam cam;
 };
 
@@ -308,7 +311,9 @@ BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, floa
 }
 
 // Closest hit in [tmin, tmax]; ties in t go to the larger DFS position (reference order).
+template <int LM = 0>
 BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Hit& h, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
   h.t = tmax;
   h.prim = -1;
@@ -326,10 +331,10 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         bool ok;
         if ((sm >> k) & 1) {
           c.sphs++;
-          ok = sph_test(S.geom[3 * pi], o, d, tmin, h.t, &t);
+          ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
         } else {
           c.tris++;
-          ok = tri_test(S.geom[3 * pi], S.geom[3 * pi + 1], S.geom[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
+          ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
         }
         if (ok && (t < h.t || pi > h.prim)) {   // t <= h.t here: t == h.t only replaces a lower DFS index
           h.t = t; h.prim = pi; h.b1 = b1; h.b2 = b2;
@@ -339,7 +344,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       ref = stack[--sp];
       continue;
     }
-    const float4* N = S.nodes + 4 * ref;
+    const float4* N = LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
     float4 a = N[0], b = N[1], cc = N[2], e = N[3];
     c.nodes += 2;
     float tnl, tfl, tnr, tfr;
@@ -367,7 +372,9 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
 }
 
 // Any hit in [tmin, tmax] (connection rays, bidirection.cpp:418-433).
+template <int LM = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
   int stack[BDPT_STACK];
   int sp = 0;
@@ -382,10 +389,10 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
         bool ok;
         if ((sm >> k) & 1) {
           c.sphs++;
-          ok = sph_test(S.geom[3 * pi], o, d, tmin, tmax, &t);
+          ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
         } else {
           c.tris++;
-          ok = tri_test(S.geom[3 * pi], S.geom[3 * pi + 1], S.geom[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+          ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
         }
         if (ok) return true;
       }
@@ -393,7 +400,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       ref = stack[--sp];
       continue;
     }
-    const float4* N = S.nodes + 4 * ref;
+    const float4* N = LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
     float4 a = N[0], b = N[1], cc = N[2], e = N[3];
     c.nodes += 2;
     float tnl, tfl, tnr, tfr;
@@ -580,7 +587,7 @@ struct SampleParams {
 
 // Subpath random walk (prepare_bidirectional_subpath, bidirection.cpp:20-102). Vertex k of the
 // reference path is written to out[k - 2]; bit k of *dmask marks delta BSDFs.
-template <int MAXV>
+template <int MAXV, int LM = 0>
 BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, float tmin, float tmax,
                         float point_pdf, float dir_pdf, f3 init_rad, f3 init_n, int max_depth, Vtx* out,
                         uint32_t* dmask) {
@@ -593,7 +600,7 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
   float rmin = tmin, rmax = tmax;
   for (;;) {
     Hit h;
-    if (!trace_closest(S, ro, rd, rmin, rmax, h, cnt)) break;
+    if (!trace_closest<LM>(S, ro, rd, rmin, rmax, h, cnt)) break;
     f3 n;
     int mat;
     shade_hit(S, h, ro, rd, &n, &mat);
@@ -862,7 +869,7 @@ BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j,
 
 // Eye and light subpaths of one pixel-sample plus their MIS constants
 // (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524).
-template <int MAXV>
+template <int MAXV, int LM = 0>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
   rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
@@ -873,7 +880,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   float dx = px / (float)sp.W, dy = py / (float)sp.H;
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   f3 rd = camera_dir(S.cam, dx, dy);
-  int ne = random_walk<MAXV>(S, g, cnt, cam, rd, S.cam.nclip, S.cam.fclip, 1.0f, 1.0f, splat3(1.0f), rd,
+  int ne = random_walk<MAXV, LM>(S, g, cnt, cam, rd, S.cam.nclip, S.cam.fclip, 1.0f, 1.0f, splat3(1.0f), rd,
                              sp.max_depth, P.E, &P.dE);
   P.nE = ne + 2;
   // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le
@@ -922,7 +929,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   }
   P.l1_dir_pdf = ldp;
   uint32_t dl = 0;
-  int nl = random_walk<MAXV>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1, &dl);
+  int nl = random_walk<MAXV, LM>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1, &dl);
   P.dL = dl;
   P.nL = nl + 2;
   eye_constants<MAXV>(S, P);

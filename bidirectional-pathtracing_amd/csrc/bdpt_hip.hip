@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -38,8 +39,9 @@ struct KParams {
   int nblocks;
   int nbx;                    // full-frame: blocks per row
   int spp_begin, spp_end, spl;
-  long long lanes_per_chunk;
-  long long nlanes;
+  unsigned nitems;            // work items = nblocks * ceil(spp_count / spl)
+  unsigned* work;             // ticket counter (zeroed before each launch)
+  int n_node4, n_geom4;       // float4 counts of the node / geometry arrays (LDS staging)
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -66,28 +68,63 @@ struct WaveQ {
   float acc[3][64];         // eye-image accumulators of the wave's 64 lanes
 };
 
+__device__ __forceinline__ float wave_sumf(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 // Resolve n (<= 64) queued connection rays, one per lane: any-hit test, then add the value of the
 // unoccluded ones to the owner's eye accumulator (LDS atomic) or splat it (global atomic).
+// Splats aimed at the flush's most common kind of target — the first splatting lane's pixel — are
+// summed across the wave first: a point light's own vertex projects to the same pixel for every
+// sample (t = 1, s = 1), and unaggregated that one address serialises ~all global atomics.
+template <int LM>
 __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int head, int n, int lane, float* light,
                                             Counters& cnt) {
+  bool vis = false;
+  float vx = 0, vy = 0, vz = 0;
+  int tgt = -1;
   if (lane < n) {
     const int k = (head + lane) & (QCAP - 1);
     f3 o = mk3(q.ox[k], q.oy[k], q.oz[k]), d = mk3(q.dx[k], q.dy[k], q.dz[k]);
-    const float tmax = q.tmax[k], vx = q.vx[k], vy = q.vy[k], vz = q.vz[k];
-    const int tgt = q.tgt[k];
-    if (!trace_any(S, o, d, BDPT_EPS_F, tmax, cnt)) {
-      if (tgt < 0) {
-        const int ow = ~tgt;
-        atomicAdd(&q.acc[0][ow], vx);
-        atomicAdd(&q.acc[1][ow], vy);
-        atomicAdd(&q.acc[2][ow], vz);
-      } else {
-        float* p = light + 3 * (size_t)tgt;
-        atomicAdd(p, vx);
-        atomicAdd(p + 1, vy);
-        atomicAdd(p + 2, vz);
-      }
+    const float tmax = q.tmax[k];
+    vx = q.vx[k]; vy = q.vy[k]; vz = q.vz[k];
+    tgt = q.tgt[k];
+    vis = !trace_any<LM>(S, o, d, BDPT_EPS_F, tmax, cnt);
+  }
+  if (vis && tgt < 0) {
+    const int ow = ~tgt;
+    atomicAdd(&q.acc[0][ow], vx);
+    atomicAdd(&q.acc[1][ow], vy);
+    atomicAdd(&q.acc[2][ow], vz);
+  }
+  const bool splat = vis && tgt >= 0;
+  const unsigned long long m = __ballot(splat);
+  if (m == 0) return;
+  const int lead = __builtin_ctzll(m);
+  const int t0 = __shfl(tgt, lead, 64);
+  const bool same = splat && tgt == t0;
+  const unsigned long long ms = __ballot(same);
+  if (__popcll(ms) > 1) {
+    const float sx = wave_sumf(same ? vx : 0.0f), sy = wave_sumf(same ? vy : 0.0f), sz = wave_sumf(same ? vz : 0.0f);
+    if (lane == lead) {
+      float* p = light + 3 * (size_t)t0;
+      atomicAdd(p, sx);
+      atomicAdd(p + 1, sy);
+      atomicAdd(p + 2, sz);
     }
+  } else if (same) {
+    float* p = light + 3 * (size_t)t0;
+    atomicAdd(p, vx);
+    atomicAdd(p + 1, vy);
+    atomicAdd(p + 2, vz);
+  }
+  if (splat && !same) {
+    float* p = light + 3 * (size_t)tgt;
+    atomicAdd(p, vx);
+    atomicAdd(p + 1, vy);
+    atomicAdd(p + 2, vz);
   }
 }
 
@@ -96,48 +133,36 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
 // mbcnt compaction) into the wave's LDS ring, and whenever 64 are queued the whole wave traces
 // them together — all 64 lanes busy on shadow rays regardless of per-lane path lengths.
-template <int MAXV, bool STATS>
 #ifndef BDPT_MIN_WAVES
 #define BDPT_MIN_WAVES 4   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
 #endif
-__global__ __launch_bounds__(128, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
-  __shared__ WaveQ qs[2];
+#ifndef BDPT_BLOCK
+#define BDPT_BLOCK 1024   // one block per CU: one LDS scene copy shared by its 16 waves
+#endif
+constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
+
+// LM (LDS mode): 0 = scene read from HBM/L2; 1 = whole BVH + geometry staged in LDS by every
+// block; 2 = the top n_top BFS-ordered nodes (the part every ray traverses) staged in LDS.
+template <int MAXV, bool STATS, int LM>
+__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
+  // One dynamic LDS array: [wave queues][optional scene / treelet copy]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  WaveQ* qs = (WaveQ*)smem;
   const int lane = threadIdx.x & 63;
   WaveQ& q = qs[threadIdx.x >> 6];
-  const long long gl = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (LM != 0) {
+    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
+    const int nn = LM == 1 ? kp.n_node4 : 4 * kp.S.ntop;
+    const int n4 = nn + (LM == 1 ? kp.n_geom4 : 0);
+    for (int k = threadIdx.x; k < n4; k += blockDim.x)
+      sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
+    __syncthreads();
+    kp.S.lnodes = sc;
+    kp.S.lgeom = sc + nn;
+  }
   Counters cnt = {0, 0, 0, 0, 0, 0};
   unsigned nsamp = 0;
-  q.acc[0][lane] = 0;
-  q.acc[1][lane] = 0;
-  q.acc[2][lane] = 0;
-  int x = 0, y = 0, s0 = 0, s1 = 0;
-  if (gl < kp.nlanes) {
-    const long long chunk = gl / kp.lanes_per_chunk;
-    const long long within = gl - chunk * kp.lanes_per_chunk;
-    const int blk = (int)(within >> 6), qq = (int)(within & 63);
-    int bx0, by0, bw, bh;
-    if (kp.blocks) {
-      int4 b = kp.blocks[blk];
-      bx0 = b.x; by0 = b.y; bw = b.z; bh = b.w;
-    } else {
-      bx0 = (blk % kp.nbx) * 8;
-      by0 = (blk / kp.nbx) * 8;
-      bw = min(8, kp.sp.W - bx0);
-      bh = min(8, kp.sp.H - by0);
-    }
-    const int qx = qq & 7, qy = qq >> 3;
-    if (qx < bw && qy < bh) {
-      x = bx0 + qx;
-      y = by0 + qy;
-      s0 = kp.spp_begin + (int)chunk * kp.spl;
-      s1 = min(s0 + kp.spl, kp.spp_end);
-    }
-  }
-  const int my_n = max(0, s1 - s0);
-  const int wave_n = wave_max(my_n);
   const float inv = 1.0f / (float)kp.sp.spp;
-  float dxs = 0, dys = 0, dzs = 0;   // direct (s = 0) eye contributions
-  int head = 0, tail = 0;            // wave-uniform ring indices
   Paths<MAXV> P;
 #ifdef BDPT_PHASE_PROF
   unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
@@ -145,81 +170,119 @@ __global__ __launch_bounds__(128, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp)
 #else
 #define PH_STAMP(v)
 #endif
-  for (int t = 0; t < wave_n; t++) {
-    Rng g;
-    int nE = 0, nL = 0;
-    PH_STAMP(tp0);
-    if (t < my_n) {
-      prepare_sample<MAXV>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
-      nE = P.nE;
-      nL = P.nL;
-      nsamp++;
+  // Persistent waves: each wave takes work items (8x8 pixel block, chunk of spl samples) from a
+  // global ticket counter until none are left, so per-item cost differences (path lengths, scene
+  // regions) never leave CUs idle at the tail of the launch. Every wave exits at the first
+  // ticket >= nitems.
+  for (;;) {
+    unsigned item = 0;
+    if (lane == 0) item = atomicAdd(kp.work, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= kp.nitems) break;
+    const int chunk = (int)(item / (unsigned)kp.nblocks);
+    const int blk = (int)(item - (unsigned)chunk * (unsigned)kp.nblocks);
+    int bx0, by0, bw, bh;
+    if (kp.blocks) {
+      int4 bb = kp.blocks[blk];
+      bx0 = bb.x; by0 = bb.y; bw = bb.z; bh = bb.w;
+    } else {
+      bx0 = (blk % kp.nbx) * 8;
+      by0 = (blk / kp.nbx) * 8;
+      bw = min(8, kp.sp.W - bx0);
+      bh = min(8, kp.sp.H - by0);
     }
-    // wave-uniform (i, j) loops: every lane is at the same strategy at the same time, so the
-    // j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
-    // for all lanes instead of interleaving with the general case.
-    const int wE = wave_max(nE), wL = wave_max(nL);
-    PH_STAMP(tp1);
-#ifdef BDPT_PHASE_PROF
-    ph_prep += tp1 - tp0;
-    unsigned long long tg0 = tp1;
-#endif
-    for (int i = 1; i < wE; i++)
-    for (int j = 0; j < wL; j++) {
-      int kind = CONN_NONE;
-      Conn cn;
-      if (i < nE && j < nL) {
-        kind = make_conn<MAXV>(kp.S, kp.sp, P, g, i, j, cn);
-        if (kind == CONN_DIRECT) {
-          dxs += cn.val.x * inv;
-          dys += cn.val.y * inv;
-          dzs += cn.val.z * inv;
+    const int qx = lane & 7, qy = lane >> 3;
+    int x = 0, y = 0, s0 = 0, s1 = 0;
+    if (qx < bw && qy < bh) {
+      x = bx0 + qx;
+      y = by0 + qy;
+      s0 = kp.spp_begin + chunk * kp.spl;
+      s1 = min(s0 + kp.spl, kp.spp_end);
+    }
+    const int my_n = max(0, s1 - s0);
+    const int wave_n = wave_max(my_n);
+    q.acc[0][lane] = 0;
+    q.acc[1][lane] = 0;
+    q.acc[2][lane] = 0;
+    float dxs = 0, dys = 0, dzs = 0;   // direct (s = 0) eye contributions
+    int head = 0, tail = 0;            // wave-uniform ring indices
+    for (int t = 0; t < wave_n; t++) {
+      Rng g;
+      int nE = 0, nL = 0;
+      PH_STAMP(tp0);
+      if (t < my_n) {
+        prepare_sample<MAXV, LM>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
+        nE = P.nE;
+        nL = P.nL;
+        nsamp++;
+      }
+      // wave-uniform (i, j) loops: every lane is at the same strategy at the same time, so the
+      // j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
+      // for all lanes instead of interleaving with the general case.
+      const int wE = wave_max(nE), wL = wave_max(nL);
+      PH_STAMP(tp1);
+  #ifdef BDPT_PHASE_PROF
+      ph_prep += tp1 - tp0;
+      unsigned long long tg0 = tp1;
+  #endif
+      for (int i = 1; i < wE; i++)
+      for (int j = 0; j < wL; j++) {
+        int kind = CONN_NONE;
+        Conn cn;
+        if (i < nE && j < nL) {
+          kind = make_conn<MAXV>(kp.S, kp.sp, P, g, i, j, cn);
+          if (kind == CONN_DIRECT) {
+            dxs += cn.val.x * inv;
+            dys += cn.val.y * inv;
+            dzs += cn.val.z * inv;
+          }
+        }
+        const bool push = kind == CONN_RAY;
+        const unsigned long long m = __ballot(push);
+        if (push) {
+          const int slot = (tail + lanes_below(m)) & (QCAP - 1);
+          q.ox[slot] = cn.o.x; q.oy[slot] = cn.o.y; q.oz[slot] = cn.o.z;
+          q.dx[slot] = cn.d.x; q.dy[slot] = cn.d.y; q.dz[slot] = cn.d.z;
+          q.tmax[slot] = cn.tmax;
+          const bool eye_t = cn.splat < 0;
+          q.vx[slot] = eye_t ? cn.val.x * inv : cn.val.x;
+          q.vy[slot] = eye_t ? cn.val.y * inv : cn.val.y;
+          q.vz[slot] = eye_t ? cn.val.z * inv : cn.val.z;
+          q.tgt[slot] = eye_t ? ~lane : cn.splat;
+        }
+        tail += __popcll(m);
+        if (tail - head >= 64) {
+          PH_STAMP(tp0);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          flush_queue<LM>(kp.S, q, head, 64, lane, kp.light, cnt);
+          __builtin_amdgcn_wave_barrier();
+          head += 64;
+          PH_STAMP(tp1);
+  #ifdef BDPT_PHASE_PROF
+          ph_flush += tp1 - tp0;
+  #endif
         }
       }
-      const bool push = kind == CONN_RAY;
-      const unsigned long long m = __ballot(push);
-      if (push) {
-        const int slot = (tail + lanes_below(m)) & (QCAP - 1);
-        q.ox[slot] = cn.o.x; q.oy[slot] = cn.o.y; q.oz[slot] = cn.o.z;
-        q.dx[slot] = cn.d.x; q.dy[slot] = cn.d.y; q.dz[slot] = cn.d.z;
-        q.tmax[slot] = cn.tmax;
-        const bool eye_t = cn.splat < 0;
-        q.vx[slot] = eye_t ? cn.val.x * inv : cn.val.x;
-        q.vy[slot] = eye_t ? cn.val.y * inv : cn.val.y;
-        q.vz[slot] = eye_t ? cn.val.z * inv : cn.val.z;
-        q.tgt[slot] = eye_t ? ~lane : cn.splat;
-      }
-      tail += __popcll(m);
-      if (tail - head >= 64) {
-        PH_STAMP(tp0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        flush_queue(kp.S, q, head, 64, lane, kp.light, cnt);
-        __builtin_amdgcn_wave_barrier();
-        head += 64;
-        PH_STAMP(tp1);
-#ifdef BDPT_PHASE_PROF
-        ph_flush += tp1 - tp0;
-#endif
-      }
+  #ifdef BDPT_PHASE_PROF
+      ph_gen += __builtin_amdgcn_s_memtime() - tg0;
+  #endif
     }
-#ifdef BDPT_PHASE_PROF
-    ph_gen += __builtin_amdgcn_s_memtime() - tg0;
-#endif
-  }
-  if (tail > head) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (tail > head) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      flush_queue<LM>(kp.S, q, head, tail - head, lane, kp.light, cnt);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    flush_queue(kp.S, q, head, tail - head, lane, kp.light, cnt);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if (my_n > 0) {
-    float ax = q.acc[0][lane] + dxs, ay = q.acc[1][lane] + dys, az = q.acc[2][lane] + dzs;
-    float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
-    if (ax != 0) atomicAdd(e, ax);
-    if (ay != 0) atomicAdd(e + 1, ay);
-    if (az != 0) atomicAdd(e + 2, az);
+    if (my_n > 0) {
+      float ax = q.acc[0][lane] + dxs, ay = q.acc[1][lane] + dys, az = q.acc[2][lane] + dzs;
+      float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
+      if (ax != 0) atomicAdd(e, ax);
+      if (ay != 0) atomicAdd(e + 1, ay);
+      if (az != 0) atomicAdd(e + 2, az);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 #ifdef BDPT_PHASE_PROF
   if (lane == 0) {
@@ -284,6 +347,7 @@ struct Ctx {
   int4* h_blocks = nullptr;   // pinned staging
   size_t h_blocks_cap = 0;
   int maxv = 5;
+  int ncu = 256;
   size_t npix = 0;
 };
 
@@ -305,18 +369,52 @@ SceneView view_of(const Ctx* c) {
   S.lights = c->d_lights;
   S.nlights = (int)c->hs.lights.size();
   S.root = c->hs.root;
+  S.lnodes = nullptr;
+  S.lgeom = nullptr;
+  S.ntop = 0;
   S.cam = c->hs.cam;
   return S;
 }
 
-template <int MAXV>
-int launch_maxv(Ctx* c, KParams& kp, unsigned grid) {
-  if (c->prm.collect_stats)
-    hipLaunchKernelGGL((k_bdpt_sample<MAXV, true>), dim3(grid), dim3(128), 0, c->stream, kp);
-  else
-    hipLaunchKernelGGL((k_bdpt_sample<MAXV, false>), dim3(grid), dim3(128), 0, c->stream, kp);
+// LDS budget for the scene copy: 160 KB per CU shared by the blocks that the 4-waves/SIMD VGPR
+// budget admits (16 waves per CU), minus their wave queues.
+constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr size_t kBlocksPerCu = 16 / kWavesPerBlock;
+constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256;
+
+// Persistent launch: as many blocks as are co-resident (occupancy query with this launch's LDS),
+// never more waves than work items.
+template <class K>
+int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BDPT_BLOCK, lds));
+  if (per_cu <= 0) { g_err = "k_bdpt_sample cannot be resident (LDS/VGPR budget)"; return BDPT_E_DEVICE; }
+  long long grid = std::min<long long>((long long)per_cu * c->ncu,
+                                       ((long long)kp.nitems + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(BDPT_BLOCK), lds, c->stream, kp);
   HIPCHK(hipGetLastError());
   return BDPT_OK;
+}
+
+template <int MAXV, bool STATS>
+int launch_lm(Ctx* c, KParams& kp) {
+  const size_t q = kWavesPerBlock * sizeof(WaveQ);
+  const size_t full = (size_t)(kp.n_node4 + kp.n_geom4) * 16;
+  const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2
+  int lm = env ? atoi(env) : (full <= kLdsSceneMax ? 1 : kp.n_node4 > 0 ? 2 : 0);
+  if (lm == 1 && full > kLdsSceneMax) lm = 2;
+  if (lm == 2) {
+    kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.n_top, kLdsSceneMax / 64);
+    if (kp.S.ntop <= 0) lm = 0;
+  }
+  if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1>, q + full, kp);
+  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2>, q + (size_t)kp.S.ntop * 64, kp);
+  return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0>, q, kp);
+}
+
+template <int MAXV>
+int launch_maxv(Ctx* c, KParams& kp) {
+  return c->prm.collect_stats ? launch_lm<MAXV, true>(c, kp) : launch_lm<MAXV, false>(c, kp);
 }
 
 void free_ctx(Ctx* c) {
@@ -372,6 +470,8 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->device = p.device;
   auto fail = [&](int code) { free_ctx(c); return code; };
   if (hipSetDevice(c->device) != hipSuccess) { g_err = "hipSetDevice failed"; return fail(BDPT_E_DEVICE); }
+  if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->ncu <= 0)
+    c->ncu = 256;
   if ((rc = upload(&c->d_nodes, c->hs.nodes))) return fail(rc);
   if ((rc = upload(&c->d_geom, c->hs.geom))) return fail(rc);
   if ((rc = upload(&c->d_shade, c->hs.shade))) return fail(rc);
@@ -440,6 +540,8 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.light = c->d_light;
   kp.stats = c->d_stats;
   kp.prof = c->d_stats + 8;
+  kp.n_node4 = (int)(c->hs.nodes.size() / 4);
+  kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);
@@ -470,23 +572,22 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   }
   int spl = c->prm.samples_per_lane;
   if (spl <= 0) {
-    // enough lanes to fill 256 CUs several times over, but >= 1 sample per lane
-    long long pix_lanes = (long long)kp.nblocks * 64;
-    long long want = 256LL * 2048;
-    spl = (int)std::max(1LL, std::min<long long>(spp_count, (pix_lanes * spp_count) / want));
+    // ~16 work items per co-resident wave (dynamic balance), as few chunks as that allows
+    const long long want = 16LL * 16 * c->ncu;
+    long long nch = std::min<long long>(spp_count, std::max(1LL, (want + kp.nblocks - 1) / kp.nblocks));
+    spl = (int)((spp_count + nch - 1) / nch);
   }
   kp.spl = spl;
   kp.spp_begin = spp_begin;
   kp.spp_end = spp_begin + spp_count;
-  int nchunks = (spp_count + spl - 1) / spl;
-  kp.lanes_per_chunk = (long long)kp.nblocks * 64;
-  kp.nlanes = kp.lanes_per_chunk * nchunks;
-  long long grid = (kp.nlanes + 127) / 128;
-  if (grid > 0x7fffffff) { g_err = "launch too large; split spp"; return BDPT_E_INVALID; }
+  const long long nchunks = (spp_count + spl - 1) / spl;
+  const long long nitems = nchunks * kp.nblocks;
+  if (nitems >= 0x7fffffffLL) { g_err = "launch too large; split spp"; return BDPT_E_INVALID; }
+  kp.nitems = (unsigned)nitems;
+  kp.work = (unsigned*)(c->d_stats + 15);
+  HIPCHK(hipMemsetAsync(kp.work, 0, sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  int rc = c->maxv == 5 ? launch_maxv<5>(c, kp, (unsigned)grid)
-         : c->maxv == 8 ? launch_maxv<8>(c, kp, (unsigned)grid)
-                        : launch_maxv<16>(c, kp, (unsigned)grid);
+  int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp) : launch_maxv<16>(c, kp);
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->timed = true;

@@ -233,17 +233,28 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
       S[10] = i2f(1);
     }
   }
-  // nodes: pre-order over internal nodes; children refs
+  // nodes: the top kTopNodes internal nodes in BFS order (the LDS treelet: every ray starts
+  // there), then the rest in DFS pre-order (subtrees contiguous for the global fetches).
   std::vector<int> dev_index(B.nodes.size(), -1);
   std::vector<int> order;
-  {
-    std::vector<int> st;
-    if (B.nodes[root].l >= 0) st.push_back(root);
+  if (B.nodes[root].l >= 0) {
+    std::vector<int> bfs{root};
+    for (size_t h = 0; h < bfs.size() && (int)order.size() < kTopNodes; h++) {
+      int id = bfs[h];
+      dev_index[id] = (int)order.size();
+      order.push_back(id);
+      for (int ch : {B.nodes[id].l, B.nodes[id].r})
+        if (B.nodes[ch].l >= 0) bfs.push_back(ch);
+    }
+    out.n_top = (int)order.size();
+    std::vector<int> st{root};
     while (!st.empty()) {
       int id = st.back();
       st.pop_back();
-      dev_index[id] = (int)order.size();
-      order.push_back(id);
+      if (dev_index[id] < 0) {
+        dev_index[id] = (int)order.size();
+        order.push_back(id);
+      }
       if (B.nodes[B.nodes[id].r].l >= 0) st.push_back(B.nodes[id].r);
       if (B.nodes[B.nodes[id].l].l >= 0) st.push_back(B.nodes[id].l);
     }

@@ -33,7 +33,10 @@ struct HostScene {
   int depth = 0;              // reference BVH depth (root = 0)
   int ref_nodes = 0;          // node count of the reference binary tree
   int nprim = 0;
+  int n_top = 0;              // leading nodes in BFS order (LDS treelet candidates)
 };
+
+constexpr int kTopNodes = 1024;
 
 // Returns BDPT_OK or an error code; err receives a message.
 int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err);

@@ -17,6 +17,7 @@ while read -r grp; do
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then grep -qi "counter" $OUT/p$i.log || { echo STOP; exit $rc; }; fi
 done <<GROUPS
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+SQ_INSTS_VALU_TRANS_F SQ_INSTS_VALU_FMA_F SQ_INSTS_VALU_MUL_F SQ_INSTS_VALU_ADD_F SQ_INSTS_VALU_INT SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VALU_CVT
 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_THREAD_CYCLES_VALU
 FETCH_SIZE
 WRITE_SIZE

@@ -20,7 +20,8 @@ if os.environ.get("BDPT_LIB"):
     B.load_library(os.environ["BDPT_LIB"])
     B._lib = B.load_library(os.environ["BDPT_LIB"])
 sc = golden_scene(scene, W, H)
-pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489)
+pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489,
+                               collect_stats=os.environ.get("BDPT_STATS") == "1")
 if os.environ.get("BDPT_WARM", "1") == "1":   # code-object load + first-launch setup, untimed
     pt.raytrace_tiles([], 0, 1)
     pt.sync()
@@ -40,4 +41,8 @@ if os.environ.get("BDPT_PHASES"):
     tot = arr[8] + arr[9] + arr[10]
     print("phase cycles (wave-summed): prepare %.3g (%.1f%%)  conn-gen %.3g (%.1f%%)  flush %.3g (%.1f%%)" % (
         arr[8], 100 * arr[8] / tot, arr[9], 100 * arr[9] / tot, arr[10], 100 * arr[10] / tot))
+if os.environ.get("BDPT_STATS") == "1":
+    st = pt.stats()
+    n = max(1, st.samples)
+    print("per sample: " + ", ".join(f"{f} {getattr(st, f) / n:.2f}" for f, _ in st._fields_))
 pt.close()
