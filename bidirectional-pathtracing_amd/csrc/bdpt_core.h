@@ -561,8 +561,8 @@ struct Vtx {
   f3 pos, n, zh, alpha;
   float woz;   // eye: (w2o*normalize(E[k-1]-E[k])).z ; light: same with L[k-1]  (f() hemisphere test)
   float fwd;   // MIS denominator of the step at this vertex (bidirection.cpp:194-211 / 257-280)
-  float q;     // rev/fwd ratio of the non-endpoint step (nom/denom with prv = next vertex outward)
-  float revg;  // g of that reverse step (needed by the s=0 special case, :181-187)
+  float gp;    // MIS prefix: G of the vertex one step inward (see mis_horner), 0 at E[2] / L[1]
+  float revg;  // g of the reverse step toward the next vertex outward (s=0 special case, :181-187)
   int mat;     // -1: no BSDF (camera / light vertex)
 };
 
@@ -619,7 +619,7 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
     v.n = n;
     v.zh = fr.Z;
     v.mat = mat;
-    v.woz = 0; v.fwd = 1; v.q = 0; v.revg = 0;
+    v.woz = 0; v.fwd = 1; v.gp = 0; v.revg = 0;
     out[count++] = v;
     if (is_delta(M.type)) dm |= 1u << i;
     if (i >= max_depth + 1 || count >= MAXV) break;
@@ -632,6 +632,18 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
   }
   *dmask = dm;
   return count;
+}
+
+// Power-heuristic sums in Horner form. Along a subpath walked from the connection endpoint
+// inward, the reference accumulates ratio_k = f_end * ... * f_k and adds ratio_k^2 when neither
+// vertex of step k is delta (t_k). Innermost first, the same sum is G_k = f_k^2 (t_k + G_{k-1});
+// every interior factor f_k is a path constant (rev/fwd pdf ratio), so G up to the vertex below
+// the endpoint is cached per vertex (Vtx::gp) and a connection costs O(1) instead of O(i + j).
+// A term whose inner sum is exactly zero stays zero (no inf * 0); the oracle's mode 2 evaluates
+// the identical expression (oracle/bdpt_oracle.cpp horner_step).
+BDPT_HD float mis_horner(float f, bool t, float g) {
+  const float s = t ? 1.0f + g : g;
+  return s == 0.0f ? 0.0f : (f * f) * s;
 }
 
 // MIS step quantities between a vertex `cur` and a neighbour `oth` whose BSDF/frame is used:
@@ -664,14 +676,18 @@ BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
       v.fwd = p * g2;
     }
   }
-  for (int k = 0; k + 1 < nh; k++) {
+  float G = 0.0f;
+  for (int k = 0; k < nh; k++) {   // vertex E[k+2]
     Vtx& v = P.E[k];
-    const Vtx& pv = P.E[k + 1];
-    f3 dw;
-    float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-    float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
-    v.revg = g;
-    v.q = (p * g) / v.fwd;
+    v.gp = G;
+    if (k + 1 < nh) {
+      const Vtx& pv = P.E[k + 1];
+      f3 dw;
+      float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
+      v.revg = g;
+      G = mis_horner((p * g) / v.fwd, !((P.dE >> (k + 1)) & 3u), G);
+    }
   }
 }
 
@@ -692,14 +708,18 @@ BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
     float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
     v.fwd = p * g2;
   }
-  for (int k = 0; k + 1 < nv; k++) {
+  float G = 0.0f;
+  for (int k = 0; k < nv; k++) {   // vertex L[k+1]
     Vtx& v = P.L[k];
-    const Vtx& pv = P.L[k + 1];
-    f3 dw;
-    float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-    float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
-    v.revg = g;
-    v.q = (p * g) / v.fwd;
+    v.gp = G;
+    if (k + 1 < nv) {
+      const Vtx& pv = P.L[k + 1];
+      f3 dw;
+      float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
+      v.revg = g;
+      G = mis_horner((p * g) / v.fwd, !((P.dL >> k) & 3u), G);
+    }
   }
 }
 
@@ -810,8 +830,10 @@ BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
 template <int MAXV>
 BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j, const LightSample& ls,
                          const EyeSample& es, int eye_light, f3 dc, float dist) {
-  float w_inv = 0.0f, ratio = 1.0f;
-  w_inv += ratio;
+#ifdef BDPT_EXP_NOMIS
+  return 0.5f;
+#endif
+  float ge = 0.0f, gl = 0.0f;
   if (i >= 2) {
     const Vtx& cur = P.E[i - 2];
     float nom;
@@ -826,23 +848,15 @@ BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j,
                        : pdf_b(S.mats[P.L[j - 1].mat], P.L[j - 1].n, pzh, dw) * 1.0f;
       nom = p * g;
     }
-    ratio *= nom / cur.fwd;
-    if (!((P.dE >> (i - 1)) & 3u)) w_inv += ratio * ratio;       // delta(E[i]) || delta(E[i-1])
-    for (int k = i - 1; k >= 2; k--) {
-      const Vtx& v = P.E[k - 2];
-      float q;
-      if (j == 0 && k == i - 1) {
-        f3 dw = normalize(sub(v.pos, cur.pos));
-        float dp = light_dir_pdf(S.lights[eye_light], neg(dw));
-        q = ((dp * 1.0f) * v.revg) / v.fwd;
-      } else {
-        q = v.q;
-      }
-      ratio *= q;
-      if (!((P.dE >> (k - 1)) & 3u)) w_inv += ratio * ratio;
+    float below = cur.gp;   // G_{i-1}
+    if (j == 0 && i >= 3) {  // the step below the emitter uses the light's dir_pdf (:224-232)
+      const Vtx& v = P.E[i - 3];
+      f3 dw = normalize(sub(v.pos, cur.pos));
+      float dp = light_dir_pdf(S.lights[eye_light], neg(dw));
+      below = mis_horner(((dp * 1.0f) * v.revg) / v.fwd, !((P.dE >> (i - 2)) & 3u), v.gp);
     }
+    ge = mis_horner(nom / cur.fwd, !((P.dE >> (i - 1)) & 3u), below);   // delta(E[i]) || delta(E[i-1])
   }
-  ratio = 1.0f;
   if (j >= 1) {
     const Vtx& cur = P.L[j - 1];
     f3 pzh = i == 1 ? es.zh : P.E[i - 2].zh;
@@ -856,15 +870,9 @@ BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j,
       g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
     }
     float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[P.E[i - 2].mat], P.E[i - 2].n, pzh, dw) * 1.0f;
-    float nom = p * g;
-    ratio *= nom / cur.fwd;
-    if (!((P.dL >> (j - 1)) & 3u)) w_inv += ratio * ratio;
-    for (int k = j - 1; k >= 1; k--) {
-      ratio *= P.L[k - 1].q;
-      if (!((P.dL >> (k - 1)) & 3u)) w_inv += ratio * ratio;
-    }
+    gl = mis_horner((p * g) / cur.fwd, !((P.dL >> (j - 1)) & 3u), cur.gp);
   }
-  return 1.0f / w_inv;
+  return 1.0f / ((1.0f + ge) + gl);
 }
 
 // Eye and light subpaths of one pixel-sample plus their MIS constants
@@ -925,7 +933,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.zh = zaxis(ln);
     v1.alpha = divs(lrad, lpp);
     v1.mat = -1;
-    v1.q = 0; v1.revg = 0; v1.woz = 0;
+    v1.gp = 0; v1.revg = 0; v1.woz = 0;
   }
   P.l1_dir_pdf = ldp;
   uint32_t dl = 0;

@@ -154,6 +154,7 @@ struct RefStreams {
 // Policies: arithmetic type + RNG source + transcendentals.
 struct PolicyRef {              // mode 0
   typedef double R;
+  static const bool kHornerMis = false;
   RefStreams* rs;
   R uS() { return rs->uS(); }
   R uG() { return rs->uG(); }
@@ -167,6 +168,7 @@ struct PolicyRef {              // mode 0
 };
 struct PolicyC64 {              // mode 1
   typedef double R;
+  static const bool kHornerMis = false;
   CounterStream* cs;
   R uS() { return (double)cs->next(); }
   R uG() { return (double)cs->next(); }
@@ -204,6 +206,9 @@ static inline void cos_sin_2pi_f32(float u, float* c, float* s) {
 
 struct PolicyC32 {              // mode 2
   typedef float R;
+  // The device sums the power-heuristic terms in Horner form over per-vertex prefixes
+  // (bdpt_core.h mis_weight); mode 2 evaluates the same factors in the same order.
+  static const bool kHornerMis = true;
   CounterStream* cs;
   R uS() { return cs->next(); }
   R uG() { return cs->next(); }
@@ -895,10 +900,19 @@ struct Tracer {
     return r;
   }
 
+  // One Horner step of the mode-2 MIS sum; a term whose inner sum is zero stays exactly zero
+  // (no inf * 0) — the same convention as the device (bdpt_core.h mis_horner).
+  static R horner_step(R f, bool t, R g) {
+    R s = t ? R(1.) + g : g;
+    return s == R(0.) ? R(0.) : (f * f) * s;
+  }
+
   R mis_weight(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L,
                const Vertex& LS, const Vertex& ES) {                          // :121-293
     R w_inv = 0., ratio = 1.;
     w_inv += ratio;
+    R fE[64], fL[64];
+    bool tE[64], tL[64];
     const Light<R>* eye_light = nullptr;
     for (int i = i_eye; i > 1; i--) {
       const Vertex& cur = E[i];
@@ -949,6 +963,11 @@ struct Tracer {
         p = bsdf_sample_pdf(nxt.isect.mat, wo, wi) * nxt.q;
       }
       denom = p * g;
+      if (P::kHornerMis) {
+        fE[i] = nom / denom;
+        tE[i] = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat));
+        continue;
+      }
       ratio *= nom / denom;
       if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
       w_inv += ratio * ratio;
@@ -981,9 +1000,21 @@ struct Tracer {
       } else {
         denom = cur.p;
       }
+      if (P::kHornerMis) {
+        fL[i] = nom / denom;
+        tL[i] = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat));
+        continue;
+      }
       ratio *= nom / denom;
       if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
       w_inv += ratio * ratio;
+    }
+    if (P::kHornerMis) {
+      // sum_k t_k (f_k ... f_end)^2 = G_end with G_k = f_k^2 (t_k + G_{k-1}), innermost vertex first
+      R ge = 0, gl = 0;
+      for (int k = 2; k <= i_eye; k++) ge = horner_step(fE[k], tE[k], ge);
+      for (int k = 1; k <= i_light; k++) gl = horner_step(fL[k], tL[k], gl);
+      return R(1.) / ((R(1.) + ge) + gl);
     }
     return R(1.) / w_inv;
   }

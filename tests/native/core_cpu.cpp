@@ -29,6 +29,9 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.lights = hs.lights.data();
   S.nlights = (int)hs.lights.size();
   S.root = hs.root;
+  S.lnodes = nullptr;
+  S.lgeom = nullptr;
+  S.ntop = 0;
   S.cam = hs.cam;
   SampleParams sp;
   sp.W = W; sp.H = H; sp.spp = spp; sp.max_depth = M; sp.seed = seed;

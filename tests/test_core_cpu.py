@@ -1,0 +1,77 @@
+"""CPU checks of the device pipeline (bdpt_core.h + bdpt_scene.cpp compiled with g++ into the
+test-only tests/native/libcorecpu.so) against the oracle's mode 2 (fp32 device semantics):
+bit-exact per-pixel eye and light images, and the product BVH's primitive order vs the
+reference's own BVH (dumped by oracle/_ref/ref_driver into tests/golden/scenes/*.json)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import bdpt_amd as B
+from _util import MODE_C32, REPO, golden_scene, oracle_render
+
+_core = None
+
+
+def core():
+    global _core
+    if _core is None:
+        import sys
+        sys.path.insert(0, REPO)
+        import __graft_entry__ as g
+        g.build_core_cpu()
+        lib = C.CDLL(g.CORE_CPU_SO)
+        P = C.POINTER(C.c_double)
+        lib.core_cpu_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int,
+                                        P, P, P]
+        lib.core_cpu_scene_info.argtypes = [C.POINTER(B.SceneDesc), C.POINTER(C.c_int),
+                                            C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        _core = lib
+    return _core
+
+
+def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None):
+    lib = core()
+    count = spp - s0 if count is None else count
+    eye = np.zeros((H, W, 3))
+    light = np.zeros((H, W, 3))
+    st = np.zeros(8)
+    d = scene.desc()
+    pd = C.POINTER(C.c_double)
+    rc = lib.core_cpu_render(C.byref(d), W, H, spp, M, seed, s0, count, None, 0,
+                             eye.ctypes.data_as(pd), light.ctypes.data_as(pd), st.ctypes.data_as(pd))
+    assert rc == 0
+    return eye, light, st
+
+
+CASES = [("CBspheres", 32, 24, 2, 5), ("CBspheres_lambertian", 32, 24, 2, 5), ("CBgems", 32, 24, 1, 7),
+         ("CBempty", 32, 24, 2, 5), ("CBspheres_refract", 24, 18, 2, 5), ("CBspheres", 24, 18, 1, 8),
+         ("CBspheres", 24, 18, 3, 1)]
+
+
+@pytest.mark.parametrize("name,W,H,spp,M", CASES)
+def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M):
+    sc = golden_scene(name, W, H)
+    eye, light, st = core_render(sc, W, H, spp, M, seed=1234)
+    _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=1234, threads=1)
+    assert np.isfinite(eye).all() and np.isfinite(light).all()
+    assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
+    assert np.array_equal(light, olight), f"light max diff {np.abs(light - olight).max()}"
+
+
+@pytest.mark.parametrize("name", ["CBspheres", "CBgems", "CBempty", "CBspheres_refract"])
+def test_product_bvh_matches_reference_bvh(name):
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "scenes", name + ".json")) as f:
+        js = json.load(f)
+    sc = golden_scene(name)
+    n = sc.desc().nprim
+    depth, ref_nodes = C.c_int(), C.c_int()
+    order = (C.c_int * n)()
+    assert core().core_cpu_scene_info(C.byref(sc.desc()), C.byref(depth), C.byref(ref_nodes), order) == 0
+    bvh = js["bvh"]
+    assert depth.value == bvh["depth"]
+    assert ref_nodes.value == bvh["nodes"]
+    assert list(order) == list(bvh["dfs_prim_order"])
