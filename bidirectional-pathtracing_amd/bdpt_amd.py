@@ -62,7 +62,8 @@ class SceneDesc(C.Structure):
 class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
                 ("max_depth", C.c_int32), ("seed", C.c_uint64), ("samples_per_lane", C.c_int32),
-                ("device", C.c_int32), ("collect_stats", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("device", C.c_int32), ("collect_stats", C.c_int32), ("pipeline", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class Tile(C.Structure):

@@ -93,18 +93,27 @@ BDPT_HD f3 to_world(const Frame& f, f3 v) { return add(add(smul(v.x, f.X), smul(
 BDPT_HD float lz(f3 v, f3 Z) { return v.x * Z.x + v.y * Z.y + v.z * Z.z; }   // (w2o*v).z
 BDPT_HD f3 to_local(const Frame& f, f3 v) { return mk3(lz(v, f.X), lz(v, f.Y), lz(v, f.Z)); }
 BDPT_HD f3 zaxis(f3 n) { return normalize(n); }   // make_coord_space(n).Z without X, Y
+BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
 
 // ------------------------------------------------------------------------------------------------
 // Counter RNG: Philox4x32-10, counter (pixel, sample, block, 0xB1D1), key (seed lo, hi).
+// Sub-streams of one pixel-sample (identical in oracle/bdpt_oracle.cpp CounterStream):
+// 0 = camera jitter + eye walk, 1 = light choice + light walk, 2 + i = the fresh light sample of
+// connection (i, j = 1). Counter = (pixel, sample, block, 0xB1D1 + (stream << 16)), so phases and
+// connections can be evaluated in any order and skipped connections consume nothing.
 struct Rng {
   uint32_t k0, k1, pix, smp;
-  uint32_t pos;   // absolute uniform index: block = pos >> 2, word = pos & 3
+  uint32_t pos;   // uniform index within the stream: block = pos >> 2, word = pos & 3
   uint32_t cur;   // block held in b0..b3 (0xffffffff: none)
+  uint32_t tag;   // 0xB1D1 + (stream << 16)
   uint32_t b0, b1, b2, b3;
 };
 BDPT_HD void rng_init(Rng& r, uint64_t seed, uint32_t pixel, uint32_t sample) {
   r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32); r.pix = pixel; r.smp = sample;
-  r.pos = 0; r.cur = 0xffffffffu;
+  r.pos = 0; r.cur = 0xffffffffu; r.tag = 0xB1D1u;
+}
+BDPT_HD void rng_stream(Rng& r, uint32_t s) {
+  r.pos = 0; r.cur = 0xffffffffu; r.tag = 0xB1D1u + (s << 16);
 }
 BDPT_HD void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -125,7 +134,7 @@ BDPT_HD float u_of(uint32_t x) { return ((float)(x >> 9) + 0.5f) * 1.19209289550
 BDPT_HD float rng_next(Rng& r) {
   const uint32_t blk = r.pos >> 2;
   if (blk != r.cur) {
-    r.b0 = r.pix; r.b1 = r.smp; r.b2 = blk; r.b3 = 0xB1D1u;
+    r.b0 = r.pix; r.b1 = r.smp; r.b2 = blk; r.b3 = r.tag;
     philox(r.b0, r.b1, r.b2, r.b3, r.k0, r.k1);
     r.cur = blk;
   }
@@ -289,6 +298,40 @@ namespace bdpt {
 #define BDPT_STACK 64
 #endif
 
+// Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
+// ones in a private array. K = 0 keeps the whole stack in the array (megakernel: its VGPR budget is
+// spent elsewhere). Near-first traversal of these trees rarely holds more than ~8 entries.
+template <int K>
+struct TravStack {
+  int s[K > 0 ? K : 1];
+  int nreg, msp;
+  int* mem;   // a separate private array, so that s[] / nreg / msp stay in registers
+  BDPT_HD explicit TravStack(int* m) : nreg(0), msp(0), mem(m) {}
+  BDPT_HD void push(int v) {
+    if (K == 0) {
+      mem[msp++] = v;
+      return;
+    }
+    if (nreg == K) mem[msp++] = s[K - 1];
+    else nreg++;
+#pragma unroll
+    for (int k = K - 1; k > 0; k--) s[k] = s[k - 1];
+    s[0] = v;
+  }
+  BDPT_HD bool pop(int& v) {
+    if (K > 0 && nreg > 0) {
+      v = s[0];
+#pragma unroll
+      for (int k = 0; k + 1 < K; k++) s[k] = s[k + 1];
+      nreg--;
+      return true;
+    }
+    if (msp == 0) return false;
+    v = mem[--msp];
+    return true;
+  }
+};
+
 struct RayInv {
   f3 o, d, inv;
 };
@@ -310,118 +353,104 @@ BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, floa
   *tf = f * 1.00000024f;
 }
 
+// Traversal loops are "while-while" (Aila & Laine 2009): an inner loop descends internal nodes
+// until this lane stands on a leaf (or its stack is empty), then the leaf's primitives are tested.
+// In a wave, every lane runs node steps together and then leaf tests together, instead of each
+// iteration paying for both code paths. Each lane visits nodes in the same near-first order as a
+// plain loop, so hits and counters do not change.
+constexpr int kTravDone = (int)0x80000000;   // not a valid leaf reference (start would be 2^24)
+
+template <int K>
+BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
+                      const float4* N, Counters& c) {
+  const float4 a = N[0], b = N[1], cc = N[2], e = N[3];
+  c.nodes += 2;
+  float tnl, tfl, tnr, tfr;
+  slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
+  slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
+  const bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
+  const bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
+  const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
+  if (hl && hr) {
+    const bool lfirst = tnl <= tnr;
+    stk.push(lfirst ? rref : lref);
+    return lfirst ? lref : rref;
+  }
+  if (hl) return lref;
+  if (hr) return rref;
+  int nx;
+  return stk.pop(nx) ? nx : kTravDone;
+}
+
+template <int LM>
+BDPT_HD const float4* node_ptr(const SceneView& S, int ref) {
+  return LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
+}
+
 // Closest hit in [tmin, tmax]; ties in t go to the larger DFS position (reference order).
-template <int LM = 0>
+template <int LM = 0, int K = 0>
 BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Hit& h, Counters& c) {
   const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
   h.t = tmax;
   h.prim = -1;
   h.b1 = 0; h.b2 = 0;
-  int stack[BDPT_STACK];
-  int sp = 0;
+  int stack_mem[BDPT_STACK];
+  TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.closest++;
   for (;;) {
-    if (ref_is_leaf(ref)) {
-      int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-      for (int k = 0; k < cnt; k++) {
-        int pi = st + k;
-        float t, b1 = 0, b2 = 0;
-        bool ok;
-        if ((sm >> k) & 1) {
-          c.sphs++;
-          ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
-        } else {
-          c.tris++;
-          ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
-        }
-        if (ok && (t < h.t || pi > h.prim)) {   // t <= h.t here: t == h.t only replaces a lower DFS index
-          h.t = t; h.prim = pi; h.b1 = b1; h.b2 = b2;
-        }
+    while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
+    if (ref == kTravDone) break;
+    const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+    for (int k = 0; k < cnt; k++) {
+      const int pi = st + k;
+      float t, b1 = 0, b2 = 0;
+      bool ok;
+      if ((sm >> k) & 1) {
+        c.sphs++;
+        ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
+      } else {
+        c.tris++;
+        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
       }
-      if (sp == 0) break;
-      ref = stack[--sp];
-      continue;
+      if (ok && (t < h.t || pi > h.prim)) {   // t <= h.t here: t == h.t only replaces a lower DFS index
+        h.t = t; h.prim = pi; h.b1 = b1; h.b2 = b2;
+      }
     }
-    const float4* N = LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
-    float4 a = N[0], b = N[1], cc = N[2], e = N[3];
-    c.nodes += 2;
-    float tnl, tfl, tnr, tfr;
-    slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
-    slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
-    bool hl = tnl <= tfl && tnl <= h.t && tfl >= tmin;
-    bool hr = tnr <= tfr && tnr <= h.t && tfr >= tmin;
-    int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
-    if (hl && hr) {
-      int nearr = tnl <= tnr ? lref : rref;
-      int farr = tnl <= tnr ? rref : lref;
-      stack[sp++] = farr;
-      ref = nearr;
-    } else if (hl) {
-      ref = lref;
-    } else if (hr) {
-      ref = rref;
-    } else {
-      if (sp == 0) break;
-      ref = stack[--sp];
-    }
+    if (!stk.pop(ref)) break;
   }
   if (h.prim >= 0) c.hits++;
   return h.prim >= 0;
 }
 
 // Any hit in [tmin, tmax] (connection rays, bidirection.cpp:418-433).
-template <int LM = 0>
+template <int LM = 0, int K = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
   const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
-  int stack[BDPT_STACK];
-  int sp = 0;
+  int stack_mem[BDPT_STACK];
+  TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.shadow++;
   for (;;) {
-    if (ref_is_leaf(ref)) {
-      int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-      for (int k = 0; k < cnt; k++) {
-        int pi = st + k;
-        float t, b1, b2;
-        bool ok;
-        if ((sm >> k) & 1) {
-          c.sphs++;
-          ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
-        } else {
-          c.tris++;
-          ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
-        }
-        if (ok) return true;
+    while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
+    if (ref == kTravDone) return false;
+    const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+    for (int k = 0; k < cnt; k++) {
+      const int pi = st + k;
+      float t, b1, b2;
+      bool ok;
+      if ((sm >> k) & 1) {
+        c.sphs++;
+        ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
+      } else {
+        c.tris++;
+        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
       }
-      if (sp == 0) return false;
-      ref = stack[--sp];
-      continue;
+      if (ok) return true;
     }
-    const float4* N = LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
-    float4 a = N[0], b = N[1], cc = N[2], e = N[3];
-    c.nodes += 2;
-    float tnl, tfl, tnr, tfr;
-    slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
-    slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
-    bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
-    bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
-    int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
-    if (hl && hr) {
-      int nearr = tnl <= tnr ? lref : rref;
-      int farr = tnl <= tnr ? rref : lref;
-      stack[sp++] = farr;
-      ref = nearr;
-    } else if (hl) {
-      ref = lref;
-    } else if (hr) {
-      ref = rref;
-    } else {
-      if (sp == 0) return false;
-      ref = stack[--sp];
-    }
+    if (!stk.pop(ref)) return false;
   }
 }
 
@@ -559,11 +588,11 @@ BDPT_HD float pdf_b(const DMat& M, f3 n, f3 zh, f3 dw) {
 // Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
 struct Vtx {
   f3 pos, n, zh, alpha;
-  float woz;   // eye: (w2o*normalize(E[k-1]-E[k])).z ; light: same with L[k-1]  (f() hemisphere test)
   float fwd;   // MIS denominator of the step at this vertex (bidirection.cpp:194-211 / 257-280)
   float gp;    // MIS prefix: G of the vertex one step inward (see mis_horner), 0 at E[2] / L[1]
-  float revg;  // g of the reverse step toward the next vertex outward (s=0 special case, :181-187)
   int mat;     // -1: no BSDF (camera / light vertex)
+  int conn;    // can receive a connection: diffuse (the only BSDF with f != 0, bsdf.cpp:52-62),
+               // seen from its front side (wo.z >= 0 toward the previous vertex), alpha != 0
 };
 
 struct LightSample {
@@ -619,7 +648,7 @@ BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, f
     v.n = n;
     v.zh = fr.Z;
     v.mat = mat;
-    v.woz = 0; v.fwd = 1; v.gp = 0; v.revg = 0;
+    v.fwd = 1; v.gp = 0; v.conn = 0;
     out[count++] = v;
     if (is_delta(M.type)) dm |= 1u << i;
     if (i >= max_depth + 1 || count >= MAXV) break;
@@ -665,7 +694,8 @@ BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
   for (int k = 0; k < nh; k++) {   // vertex E[k+2]
     Vtx& v = P.E[k];
     f3 prevp = k == 0 ? cam : P.E[k - 1].pos;
-    v.woz = lz(normalize(sub(prevp, v.pos)), v.zh);
+    v.conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(prevp, v.pos)), v.zh) >= 0 &&
+             nonzero3(v.alpha);
     if (k == 0) {
       v.fwd = 1.0f * 1.0f;
     } else {
@@ -685,7 +715,6 @@ BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
       f3 dw;
       float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
       float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
-      v.revg = g;
       G = mis_horner((p * g) / v.fwd, !((P.dE >> (k + 1)) & 3u), G);
     }
   }
@@ -698,11 +727,12 @@ BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
     Vtx& v = P.L[k];
     if (k == 0) {
       v.fwd = l1_p;
-      v.woz = 0;
+      v.conn = 0;
       continue;
     }
     const Vtx& nx = P.L[k - 1];
-    v.woz = lz(normalize(sub(nx.pos, v.pos)), v.zh);
+    v.conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(nx.pos, v.pos)), v.zh) >= 0 &&
+             nonzero3(v.alpha);
     f3 dw;
     float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
     float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
@@ -717,7 +747,6 @@ BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
       f3 dw;
       float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
       float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
-      v.revg = g;
       G = mis_horner((p * g) / v.fwd, !((P.dL >> k) & 3u), G);
     }
   }
@@ -821,59 +850,71 @@ BDPT_HD EyeSample camera_sample(const DCam& c, int W, int H, f3 p) {
   return e;
 }
 
-BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
 
 // multiple_importance_sampling_weight (bidirection.cpp:121-293) with cached path constants.
+// PA: path accessor — e(k) / l(k) return reference vertices E[k] (k >= 2) / L[k] (k >= 1) and
+// dE / dL the delta masks; PathsInRegs below (one lane's Paths) or the wavefront vertex store.
 // i, j: reference vertex indices; ls: fresh light sample (j == 1); es: camera sample (i == 1);
 // dc, dist: normalize(vl - ve) and |vl - ve| of the connection (j >= 1), which are exactly the
 // endpoint-step directions the reference recomputes (normalize(-v) == -normalize(v) in IEEE).
-template <int MAXV>
-BDPT_HD float mis_weight(const SceneView& S, const Paths<MAXV>& P, int i, int j, const LightSample& ls,
-                         const EyeSample& es, int eye_light, f3 dc, float dist) {
+template <class PA>
+BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const Vtx* lv, int i, int j,
+                         const LightSample& ls, const EyeSample& es, int eye_light, f3 dc, float dist) {
 #ifdef BDPT_EXP_NOMIS
   return 0.5f;
 #endif
   float ge = 0.0f, gl = 0.0f;
   if (i >= 2) {
-    const Vtx& cur = P.E[i - 2];
+    const Vtx& cur = *ev;
     float nom;
     if (j == 0) {
       float p = S.lights[eye_light].type == LIGHT_POINT ? 1.0f : 1.0f / S.lights[eye_light].area;
       nom = p * 1.0f;
     } else {
-      f3 pzh = j == 1 ? ls.zh : P.L[j - 1].zh;
+      f3 pzh = j == 1 ? ls.zh : lv->zh;
       f3 dw = neg(dc);   // normalize(E[i] - vl)
       float g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
-      float p = j == 1 ? ls.dir_pdf * 1.0f
-                       : pdf_b(S.mats[P.L[j - 1].mat], P.L[j - 1].n, pzh, dw) * 1.0f;
+      float p = j == 1 ? ls.dir_pdf * 1.0f : pdf_b(S.mats[lv->mat], lv->n, pzh, dw) * 1.0f;
       nom = p * g;
     }
     float below = cur.gp;   // G_{i-1}
     if (j == 0 && i >= 3) {  // the step below the emitter uses the light's dir_pdf (:224-232)
-      const Vtx& v = P.E[i - 3];
+      const Vtx v = P.e(i - 1);
+      f3 dr;
+      const float revg = step_g(v.pos, v.n, cur.pos, cur.zh, &dr);   // g of the step E[i-1] <- E[i]
       f3 dw = normalize(sub(v.pos, cur.pos));
       float dp = light_dir_pdf(S.lights[eye_light], neg(dw));
-      below = mis_horner(((dp * 1.0f) * v.revg) / v.fwd, !((P.dE >> (i - 2)) & 3u), v.gp);
+      below = mis_horner(((dp * 1.0f) * revg) / v.fwd, !((P.dE >> (i - 2)) & 3u), v.gp);
     }
     ge = mis_horner(nom / cur.fwd, !((P.dE >> (i - 1)) & 3u), below);   // delta(E[i]) || delta(E[i-1])
   }
   if (j >= 1) {
-    const Vtx& cur = P.L[j - 1];
-    f3 pzh = i == 1 ? es.zh : P.E[i - 2].zh;
+    const Vtx& cur = *lv;   // j == 1: the original L[1], not the fresh sample (quirk 5)
+    f3 pzh = i == 1 ? es.zh : ev->zh;
     f3 dw;
     float g;
     if (j >= 2) {   // cur = L[j] = vl: normalize(L[j] - ve) = dc
       dw = dc;
       g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
-    } else {        // cur = the original L[1], not the fresh sample (quirk 5)
-      f3 ppos = i == 1 ? es.pos : P.E[i - 2].pos;
+    } else {
+      f3 ppos = i == 1 ? es.pos : ev->pos;
       g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
     }
-    float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[P.E[i - 2].mat], P.E[i - 2].n, pzh, dw) * 1.0f;
+    float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[ev->mat], ev->n, pzh, dw) * 1.0f;
     gl = mis_horner((p * g) / cur.fwd, !((P.dL >> (j - 1)) & 3u), cur.gp);
   }
   return 1.0f / ((1.0f + ge) + gl);
 }
+
+// Path accessor over one lane's Paths (megakernel, host tests).
+template <int MAXV>
+struct PathsInRegs {
+  const Paths<MAXV>& P;
+  uint32_t dE, dL;
+  BDPT_HD explicit PathsInRegs(const Paths<MAXV>& p) : P(p), dE(p.dE), dL(p.dL) {}
+  BDPT_HD Vtx e(int k) const { return P.E[k - 2]; }
+  BDPT_HD Vtx l(int k) const { return P.L[k - 1]; }
+};
 
 // Eye and light subpaths of one pixel-sample plus their MIS constants
 // (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524).
@@ -892,6 +933,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
                              sp.max_depth, P.E, &P.dE);
   P.nE = ne + 2;
   // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le
+  rng_stream(g, 1);
   int lid = (int)(rng_next(g) * (float)S.nlights);
   if (lid >= S.nlights) lid = S.nlights - 1;
   const DLight& L0 = S.lights[lid];
@@ -933,7 +975,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.zh = zaxis(ln);
     v1.alpha = divs(lrad, lpp);
     v1.mat = -1;
-    v1.gp = 0; v1.revg = 0; v1.woz = 0;
+    v1.gp = 0; v1.conn = 0;
   }
   P.l1_dir_pdf = ldp;
   uint32_t dl = 0;
@@ -957,68 +999,52 @@ struct Conn {
 
 // A vertex that can receive a connection: diffuse (f != 0 only for DiffuseBSDF, bsdf.cpp:52-62),
 // viewed from its front side (wo.z >= 0) and carrying throughput.
-BDPT_HD bool can_connect(const SceneView& S, const Vtx& v) {
-  return S.mats[v.mat].type == MAT_DIFFUSE && v.woz >= 0 && nonzero3(v.alpha);
-}
-// Uniforms consumed by the fresh light sample of a j == 1 connection (rand_light + sample_Le_point).
-BDPT_HD void skip_light_sample(const SceneView& S, Rng& g) {
-  if (S.nlights == 1) {
-    rng_skip(g, S.lights[0].type == LIGHT_POINT ? 1u : 3u);
-    return;
-  }
-  int id = (int)(rng_next(g) * (float)S.nlights);
-  if (id >= S.nlights) id = S.nlights - 1;
-  if (S.lights[id].type != LIGHT_POINT) rng_skip(g, 2);
-}
-
-template <int MAXV>
-BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const Paths<MAXV>& P, Rng& g, int i, int j,
-                      Conn& cn) {
+BDPT_HD bool can_connect(const Vtx& v) { return v.conn != 0; }
+template <class PA>
+BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   const bool eye_cam = i == 1;
-  const Vtx* ev = eye_cam ? nullptr : &P.E[i - 2];
+  Vtx ev, lv;
   LightSample ls;
   EyeSample es;
   es.x = -1; es.y = -1;
   cn.splat = -1;
+  if (!eye_cam) ev = P.e(i);
   if (j == 0) {
     if (eye_cam) return CONN_NONE;
-    const DMat& M = S.mats[ev->mat];
+    const DMat& M = S.mats[ev.mat];
     if (M.type != MAT_EMISSION) return CONN_NONE;
     f3 c = mk3(M.a[0], M.a[1], M.a[2]);
     if (!(norm(c) > BDPT_EPS_F)) return CONN_NONE;
     int eye_light = -1;
     for (int l = 0; l < S.nlights; l++)
-      if (light_contains(S.lights[l], ev->pos)) { eye_light = l; break; }
+      if (light_contains(S.lights[l], ev.pos)) { eye_light = l; break; }
     if (eye_light < 0) return CONN_NONE;
-    f3 prevp = i == 2 ? cam : P.E[i - 3].pos;
-    f3 wi = normalize(sub(ev->pos, prevp));
+    f3 prevp = i == 2 ? cam : P.e(i - 1).pos;
+    f3 wi = normalize(sub(ev.pos, prevp));
     const DLight& EL = S.lights[eye_light];
     if (!(light_dir_pdf(EL, wi) > 0)) return CONN_NONE;
     c = mk3(EL.rad[0], EL.rad[1], EL.rad[2]);
-    f3 contrib = mul(mul(ev->alpha, splat3(1.0f)), c);
+    f3 contrib = mul(mul(ev.alpha, splat3(1.0f)), c);
     float w = 0;
-    if (norm(contrib) > BDPT_EPS_F) w = mis_weight<MAXV>(S, P, i, 0, ls, es, eye_light, splat3(0), 0);
+    if (norm(contrib) > BDPT_EPS_F) w = mis_weight(S, P, &ev, &lv, i, 0, ls, es, eye_light, splat3(0), 0);
     cn.val = muls(contrib, w);
     return CONN_DIRECT;
   }
-  // Zero-contribution connections (f_eye = 0 or f_light = 0 or zero throughput) end here; only
-  // the RNG draws of a fresh light sample (j == 1) must still happen.
-  if (!eye_cam && !can_connect(S, *ev)) {
-    if (j == 1) skip_light_sample(S, g);
-    return CONN_NONE;
-  }
-  if (j >= 2 && !can_connect(S, P.L[j - 1])) return CONN_NONE;
+  // Zero-contribution connections (f_eye = 0 or f_light = 0 or zero throughput) end here.
+  if (!eye_cam && !can_connect(ev)) return CONN_NONE;
+  lv = P.l(j);   // j == 1: the original L[1] (MIS quirk); j >= 2: the light endpoint
+  if (j >= 2 && !can_connect(lv)) return CONN_NONE;
   f3 vl_pos, vl_n, la;
   if (j == 1) {   // fresh light sample (bidirection.cpp:332-358)
-    const f3 epos = eye_cam ? cam : ev->pos;
+    const f3 epos = eye_cam ? cam : ev.pos;
+    rng_stream(g, 2u + (uint32_t)i);
     int id = (int)(rng_next(g) * (float)S.nlights);
     if (id >= S.nlights) id = S.nlights - 1;
     float lp;
     ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
     vl_pos = ls.pos; vl_n = ls.n; la = ls.alpha;
   } else {
-    const Vtx& lv = P.L[j - 1];
     vl_pos = lv.pos; vl_n = lv.n; la = lv.alpha;
   }
   f3 ve_pos, ve_n, ea;
@@ -1027,7 +1053,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const Paths<MA
     if (!(es.x >= 0 && es.y >= 0 && es.x < sp.W && es.y < sp.H)) return CONN_NONE;   // not splatted
     ve_pos = es.pos; ve_n = es.n; ea = es.alpha;
   } else {
-    ve_pos = ev->pos; ve_n = ev->n; ea = ev->alpha;
+    ve_pos = ev.pos; ve_n = ev.n; ea = ev.alpha;
   }
   f3 eal = mul(ea, la);
   if (!nonzero3(eal)) return CONN_NONE;
@@ -1037,12 +1063,11 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const Paths<MA
   dc = normalize(dc);
   f3 f_eye = splat3(1.0f), f_light = splat3(1.0f);
   if (!eye_cam) {
-    if (lz(dc, ev->zh) < 0) return CONN_NONE;   // f_eye = 0 (bsdf.cpp:56-58)
-    const DMat& M = S.mats[ev->mat];
+    if (lz(dc, ev.zh) < 0) return CONN_NONE;   // f_eye = 0 (bsdf.cpp:56-58)
+    const DMat& M = S.mats[ev.mat];
     f_eye = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
   }
   if (j >= 2) {
-    const Vtx& lv = P.L[j - 1];
     if (lz(neg(dc), lv.zh) < 0) return CONN_NONE;   // f_light = 0
     const DMat& M = S.mats[lv.mat];
     f_light = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
@@ -1051,7 +1076,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const Paths<MA
   f3 c = mul(muls(f_eye, gg), f_light);
   f3 contrib = mul(eal, c);
   if (!(norm(contrib) > BDPT_EPS_F)) return CONN_NONE;   // w = 0
-  float w = mis_weight<MAXV>(S, P, i, j, ls, es, -1, dc, dist);
+  float w = mis_weight(S, P, &ev, &lv, i, j, ls, es, -1, dc, dist);
   f3 ill = muls(contrib, w);
   cn.o = ve_pos;
   cn.d = dc;
@@ -1076,7 +1101,7 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
   for (int i = 1; i < P.nE; i++) {
     for (int j = 0; j < P.nL; j++) {
       Conn cn;
-      int kind = make_conn<MAXV>(S, sp, P, g, i, j, cn);
+      int kind = make_conn(S, sp, PathsInRegs<MAXV>(P), g, i, j, cn);
       if (kind == CONN_DIRECT) {
         eye_sum = add(eye_sum, cn.val);
       } else if (kind == CONN_RAY) {

@@ -1,0 +1,79 @@
+// bdpt_ctx.h — the device context behind the C-ABI handle (shared by the megakernel TU,
+// bdpt_hip.hip, and the wavefront pipeline, bdpt_wavefront.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "bdpt/bdpt.h"
+#include "bdpt_core.h"
+#include "bdpt_scene.h"
+
+namespace bdpt {
+
+extern thread_local std::string g_err;   // bdpt_last_error()
+
+struct WfState;   // wavefront buffers (bdpt_wavefront.hip)
+
+enum { PIPE_WAVEFRONT = 0, PIPE_MEGAKERNEL = 1 };
+
+struct Ctx {
+  HostScene hs;
+  bdpt_params prm;
+  int device = 0;
+  int pipeline = PIPE_WAVEFRONT;
+  hipStream_t own = nullptr, stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  float* d_nodes = nullptr;
+  float* d_geom = nullptr;
+  float* d_shade = nullptr;
+  DMat* d_mats = nullptr;
+  DLight* d_lights = nullptr;
+  int* d_prim_ref = nullptr;
+  float* d_eye = nullptr;
+  float* d_light = nullptr;
+  float* d_sample = nullptr;
+  unsigned long long* d_stats = nullptr;   // [0..6] counters, [8..10] phase cycles, [15] tickets
+  int4* d_blocks = nullptr;
+  size_t blocks_cap = 0;
+  int4* h_blocks = nullptr;   // pinned staging
+  size_t h_blocks_cap = 0;
+  int maxv = 5;
+  int ncu = 256;
+  size_t npix = 0;
+  WfState* wf = nullptr;
+};
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      ::bdpt::g_err = std::string(#x) + ": " + hipGetErrorString(e_);               \
+      return BDPT_E_DEVICE;                                                         \
+    }                                                                               \
+  } while (0)
+
+inline SceneView view_of(const Ctx* c) {
+  SceneView S;
+  S.nodes = (const float4*)c->d_nodes;
+  S.geom = (const float4*)c->d_geom;
+  S.shade = (const float4*)c->d_shade;
+  S.mats = c->d_mats;
+  S.lights = c->d_lights;
+  S.nlights = (int)c->hs.lights.size();
+  S.root = c->hs.root;
+  S.lnodes = nullptr;
+  S.lgeom = nullptr;
+  S.ntop = 0;
+  S.cam = c->hs.cam;
+  return S;
+}
+
+// Wavefront pipeline (bdpt_wavefront.hip). blocks: device list of 8x8 pixel blocks (x0, y0, w, h)
+// or null for the full frame (nbx blocks per row).
+int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, int spp_count);
+void wf_free(Ctx* c);
+
+}  // namespace bdpt

@@ -20,13 +20,14 @@
 
 #include "bdpt/bdpt.h"
 #include "bdpt_core.h"
+#include "bdpt_ctx.h"
 #include "bdpt_scene.h"
 
 using namespace bdpt;
 
-namespace {
+thread_local std::string bdpt::g_err;
 
-thread_local std::string g_err;
+namespace {
 
 struct KParams {
   SceneView S;
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
         int kind = CONN_NONE;
         Conn cn;
         if (i < nE && j < nL) {
-          kind = make_conn<MAXV>(kp.S, kp.sp, P, g, i, j, cn);
+          kind = make_conn(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn);
           if (kind == CONN_DIRECT) {
             dxs += cn.val.x * inv;
             dys += cn.val.y * inv;
@@ -325,57 +326,6 @@ __global__ void k_combine(const float* a, const float* b, float* out, long long 
   if (i < n) out[i] = a[i] + b[i];
 }
 
-struct Ctx {
-  HostScene hs;
-  bdpt_params prm;
-  int device = 0;
-  hipStream_t own = nullptr, stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
-  float* d_nodes = nullptr;
-  float* d_geom = nullptr;
-  float* d_shade = nullptr;
-  DMat* d_mats = nullptr;
-  DLight* d_lights = nullptr;
-  int* d_prim_ref = nullptr;
-  float* d_eye = nullptr;
-  float* d_light = nullptr;
-  float* d_sample = nullptr;
-  unsigned long long* d_stats = nullptr;
-  int4* d_blocks = nullptr;
-  size_t blocks_cap = 0;
-  int4* h_blocks = nullptr;   // pinned staging
-  size_t h_blocks_cap = 0;
-  int maxv = 5;
-  int ncu = 256;
-  size_t npix = 0;
-};
-
-#define HIPCHK(x)                                                                   \
-  do {                                                                              \
-    hipError_t e_ = (x);                                                            \
-    if (e_ != hipSuccess) {                                                         \
-      g_err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
-      return BDPT_E_DEVICE;                                                         \
-    }                                                                               \
-  } while (0)
-
-SceneView view_of(const Ctx* c) {
-  SceneView S;
-  S.nodes = (const float4*)c->d_nodes;
-  S.geom = (const float4*)c->d_geom;
-  S.shade = (const float4*)c->d_shade;
-  S.mats = c->d_mats;
-  S.lights = c->d_lights;
-  S.nlights = (int)c->hs.lights.size();
-  S.root = c->hs.root;
-  S.lnodes = nullptr;
-  S.lgeom = nullptr;
-  S.ntop = 0;
-  S.cam = c->hs.cam;
-  return S;
-}
-
 // LDS budget for the scene copy: 160 KB per CU shared by the blocks that the 4-waves/SIMD VGPR
 // budget admits (16 waves per CU), minus their wave queues.
 constexpr size_t kLdsPerCu = 160 * 1024;
@@ -423,6 +373,7 @@ void free_ctx(Ctx* c) {
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  wf_free(c);
   if (c->h_blocks) (void)hipHostFree(c->h_blocks);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -458,6 +409,8 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   Ctx* c = new Ctx();
   c->prm = p;
   c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : 16;
+  c->pipeline = p.pipeline == 1 ? PIPE_MEGAKERNEL : PIPE_WAVEFRONT;
+  if (const char* pe = getenv("BDPT_PIPELINE")) c->pipeline = atoi(pe) == 1 ? PIPE_MEGAKERNEL : PIPE_WAVEFRONT;
   int rc = build_host_scene(scene, c->hs, g_err);
   if (rc) { delete c; return rc; }
   int ndev = 0;
@@ -569,6 +522,14 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
     HIPCHK(hipMemcpyAsync(c->d_blocks, c->h_blocks, blk.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
     kp.blocks = c->d_blocks;
     kp.nblocks = (int)blk.size();
+  }
+  if (c->pipeline == PIPE_WAVEFRONT) {
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    int rc = wf_render(c, kp.blocks, kp.nblocks, kp.nbx, spp_begin, spp_count);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return BDPT_OK;
   }
   int spl = c->prm.samples_per_lane;
   if (spl <= 0) {

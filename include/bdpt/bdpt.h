@@ -110,7 +110,8 @@ typedef struct bdpt_params {
   int32_t samples_per_lane;   /* 0 = auto                                                 */
   int32_t device;             /* HIP device ordinal                                       */
   int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
-  int32_t reserved[5];
+  int32_t pipeline;           /* 0 = wavefront (default), 1 = megakernel; same results    */
+  int32_t reserved[4];
 } bdpt_params;
 
 typedef struct bdpt_tile {

@@ -122,16 +122,21 @@ inline void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1) {
 // u = ((x >> 9) + 0.5) * 2^-23 : exact in fp32 (24 significant bits), in [2^-24, 1 - 2^-24].
 inline float u24(uint32_t x) { return ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-07f; }
 
+// Counter modes: every pixel-sample owns independent sub-streams, so the device can run its
+// phases in any order: 0 = camera jitter + eye walk, 1 = light choice + light walk,
+// 2 + i = the fresh light sample of connection (i, j = 1) (bidirection.cpp:332-358).
+// Counter = (pixel, sample, block, 0xB1D1 + (stream << 16)).
 struct CounterStream {
-  uint32_t k0, k1, pix, smp, block;
+  uint32_t k0, k1, pix, smp, block, tag;
   uint32_t buf[4];
   int idx;
   void init(uint64_t seed, uint32_t pixel, uint32_t sample) {
-    k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); pix = pixel; smp = sample; block = 0; idx = 4;
+    k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); pix = pixel; smp = sample; block = 0; idx = 4; tag = 0;
   }
+  void select(uint32_t s) { tag = s; block = 0; idx = 4; }
   float next() {
     if (idx == 4) {
-      buf[0] = pix; buf[1] = smp; buf[2] = block++; buf[3] = 0xB1D1u;
+      buf[0] = pix; buf[1] = smp; buf[2] = block++; buf[3] = 0xB1D1u + (tag << 16);
       philox4x32_10(buf, k0, k1);
       idx = 0;
     }
@@ -159,6 +164,7 @@ struct PolicyRef {              // mode 0
   R uS() { return rs->uS(); }
   R uG() { return rs->uG(); }
   int rand_light(int n) { return 0 + std::rand() % (n - 1 - 0 + 1); }   // sampler.h:25-28
+  void stream(uint32_t) {}                                                  // one sequential stream
   static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
   static R cos_acos(R z) { return std::cos(std::acos(z)); }
   static R pow2(R x) { return std::pow(x, 2); }
@@ -173,6 +179,7 @@ struct PolicyC64 {              // mode 1
   R uS() { return (double)cs->next(); }
   R uG() { return (double)cs->next(); }
   int rand_light(int n) { int k = (int)((double)cs->next() * n); return k < n ? k : n - 1; }
+  void stream(uint32_t k) { cs->select(k); }
   static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
   static R cos_acos(R z) { return std::cos(std::acos(z)); }
   static R pow2(R x) { return std::pow(x, 2); }
@@ -213,6 +220,7 @@ struct PolicyC32 {              // mode 2
   R uS() { return cs->next(); }
   R uG() { return cs->next(); }
   int rand_light(int n) { int k = (int)(cs->next() * (float)n); return k < n ? k : n - 1; }
+  void stream(uint32_t k) { cs->select(k); }
   static void cos_sin_2pi(R xi, R* c, R* s) { cos_sin_2pi_f32(xi, c, s); }
   static R cos_acos(R z) { return z; }
   static R pow2(R x) { return x * x; }
@@ -1053,6 +1061,7 @@ struct Tracer {
     } else {
       V f_eye, f_light, connect;
       if (i_light == 1) {
+        pol.stream(2u + (uint32_t)i_eye);
         int n = (int)sc.lights.size();
         int id = pol.rand_light(n);
         V ldir, lpoint, ln;
@@ -1157,6 +1166,7 @@ struct Tracer {
     prepare_subpath(r, 1., 1., E, V(1., 1., 1.), r.d, false);
     R lpp, ldp;
     V lrad, ln;
+    pol.stream(1);
     Ray<R> lr = sample_light_ray(lpp, ldp, lrad, ln);
     prepare_subpath(lr, lpp, ldp, L, lrad, ln, true);
 #ifdef ORC_DEBUG2
