@@ -70,6 +70,9 @@ class Tile(C.Structure):
     _fields_ = [("x0", C.c_int32), ("y0", C.c_int32), ("w", C.c_int32), ("h", C.c_int32)]
 
 
+PIPELINE_AUTO, PIPELINE_MEGAKERNEL, PIPELINE_WAVEFRONT = 0, 1, 2
+
+
 class Stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("closest_rays", C.c_uint64),
                 ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
@@ -181,6 +184,32 @@ def scene_from_json(js) -> Scene:
     return Scene(ptype, geom, pmat, mats, lights, cam, cam.get("screenW", 0), cam.get("screenH", 0))
 
 
+def load_dae(path: str, width: int = 0, height: int = 0, dump_json: str = None) -> Scene:
+    """Scene from a COLLADA file through the library's host loader (bdpt_dae_load: ColladaParser
+    + Application::load semantics). width/height > 0 apply the -r W H camera retarget."""
+    lib = load_library()
+    h = C.c_void_p()
+    _check(lib.bdpt_dae_load(os.fsencode(path), width, height, C.byref(h)), lib)
+    try:
+        if dump_json:
+            _check(lib.bdpt_dae_dump_json(h, os.fsencode(dump_json)), lib)
+        d = SceneDesc()
+        _check(lib.bdpt_dae_get_desc(h, C.byref(d)), lib)
+        n = d.nprim
+        ptype = np.ctypeslib.as_array(d.prim_type, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+        geom = np.ctypeslib.as_array(d.prim_geom, shape=(n * 18,)).copy() if n else np.zeros(0)
+        pmat = np.ctypeslib.as_array(d.prim_mat, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+        mats = [Material.from_buffer_copy(d.mats[i]) for i in range(d.nmat)]
+        lights = [Light.from_buffer_copy(d.lights[i]) for i in range(d.nlight)]
+        c = d.camera
+        cam = {"pos": list(c.pos), "c2w_cols": [list(c.c2w[3 * k:3 * k + 3]) for k in range(3)],
+               "w2c_cols": [list(c.w2c[3 * k:3 * k + 3]) for k in range(3)],
+               "hFov": c.hfov_deg, "vFov": c.vfov_deg, "nClip": c.nclip, "fClip": c.fclip}
+        return Scene(ptype, geom, pmat, mats, lights, cam, width, height)
+    finally:
+        lib.bdpt_dae_free(h)
+
+
 def retarget_camera(scene: Scene, width: int, height: int) -> Scene:
     """Camera::set_screen_size (camera.cpp:83-89): screenDist fixed, FOV follows the frame size
     (the reference's FOV quirk)."""
@@ -224,6 +253,11 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
     lib.bdpt_trace_rays.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_int32,
                                     C.POINTER(C.c_float), C.POINTER(C.c_int32)]
+    lib.bdpt_dae_load.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bdpt_dae_get_desc.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    lib.bdpt_dae_dump_json.argtypes = [C.c_void_p, C.c_char_p]
+    lib.bdpt_dae_free.argtypes = [C.c_void_p]
+    lib.bdpt_dae_free.restype = None
     if path is None:
         _lib = lib
     return lib
@@ -245,7 +279,7 @@ class BidirectionalPathTracer:
 
     def __init__(self, scene: Scene, width: int, height: int, spp: int, max_depth: int,
                  seed: int = 5489, device: int = 0, samples_per_lane: int = 0,
-                 collect_stats: bool = False):
+                 collect_stats: bool = False, pipeline: int = PIPELINE_AUTO):
         self.lib = load_library()
         self.scene = scene
         self.width, self.height, self.spp, self.max_depth = width, height, spp, max_depth
@@ -253,6 +287,7 @@ class BidirectionalPathTracer:
         p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
         p.seed, p.samples_per_lane, p.device = seed, samples_per_lane, device
         p.collect_stats = 1 if collect_stats else 0
+        p.pipeline = pipeline
         self._desc = scene.desc()
         ctx = C.c_void_p()
         _check(self.lib.bdpt_create(C.byref(self._desc), C.byref(p), C.byref(ctx)), self.lib)

@@ -8,11 +8,12 @@
 
 #include "bdpt/bdpt.h"
 #include "bdpt_core.h"
+#include "bdpt_err.h"
 #include "bdpt_scene.h"
 
 namespace bdpt {
 
-extern thread_local std::string g_err;   // bdpt_last_error()
+// bdpt_last_error() text: bdpt_err.h
 
 struct WfState;   // wavefront buffers (bdpt_wavefront.hip)
 

@@ -409,8 +409,11 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   Ctx* c = new Ctx();
   c->prm = p;
   c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : 16;
-  c->pipeline = p.pipeline == 1 ? PIPE_MEGAKERNEL : PIPE_WAVEFRONT;
-  if (const char* pe = getenv("BDPT_PIPELINE")) c->pipeline = atoi(pe) == 1 ? PIPE_MEGAKERNEL : PIPE_WAVEFRONT;
+  // 0 = auto: the megakernel (measured faster on the reference's Cornell-box scenes), 1 =
+  // megakernel, 2 = wavefront. BDPT_PIPELINE overrides (diagnostics / A-B runs).
+  int pipe = p.pipeline;
+  if (const char* pe = getenv("BDPT_PIPELINE")) pipe = atoi(pe);
+  c->pipeline = pipe == 2 ? PIPE_WAVEFRONT : PIPE_MEGAKERNEL;
   int rc = build_host_scene(scene, c->hs, g_err);
   if (rc) { delete c; return rc; }
   int ndev = 0;

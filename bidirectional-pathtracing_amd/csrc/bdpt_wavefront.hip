@@ -58,7 +58,8 @@ struct WfParams {
   float* light;
   unsigned long long* stats;
   const int4* blocks;
-  int nblocks, nbx;
+  int nblocks, nbx;       // blocks of this batch (a window of the render's block list)
+  int block0;             // first block of the window
   int batch_s0, spp_end;
   unsigned nslots;        // active slots of this batch
   unsigned stride;        // allocated slots (vertex-store stride)
@@ -162,7 +163,7 @@ __device__ __forceinline__ void flush_stats(unsigned long long* st, unsigned sam
 __device__ __forceinline__ bool slot_pixel(const WfParams& p, unsigned slot, int& x, int& y, int& smp) {
   const unsigned per = (unsigned)p.nblocks * 64u;
   const unsigned k = slot / per, rem = slot - k * per;
-  const int blk = (int)(rem >> 6), q = (int)(rem & 63u);
+  const int blk = p.block0 + (int)(rem >> 6), q = (int)(rem & 63u);
   int bx0, by0, bw, bh;
   if (p.blocks) {
     const int4 b = p.blocks[blk];
@@ -748,16 +749,16 @@ int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, i
   p.n_geom4 = (int)(c->hs.geom.size() / 4);
   p.inv_spp = 1.0f / (float)c->prm.spp;
   for (const DLight& l : c->hs.lights) p.point_light |= l.type == LIGHT_POINT;
-  const long long per_sample = (long long)nblocks * 64;
-  if (per_sample > (long long)w->stride) {
-    g_err = "tile list larger than one wavefront batch (raise BDPT_WF_SLOTS)";
-    return BDPT_E_UNSUPPORTED;
-  }
-  const int K = (int)std::max<long long>(1, w->stride / per_sample);
+  // a batch = a window of <= stride/64 blocks x K samples
+  const int win = (int)std::min<long long>(nblocks, w->stride / 64);
+  const int K = (int)std::max<long long>(1, w->stride / ((long long)win * 64));
+  for (int b0 = 0; b0 < nblocks; b0 += win)
   for (int s0 = spp_begin; s0 < p.spp_end; s0 += K) {
     const int k = std::min(K, p.spp_end - s0);
+    p.block0 = b0;
+    p.nblocks = std::min(win, nblocks - b0);
     p.batch_s0 = s0;
-    p.nslots = (unsigned)(k * per_sample);
+    p.nslots = (unsigned)((long long)k * p.nblocks * 64);
     HIPCHK(hipMemsetAsync(w->ctr, 0, (size_t)(Q_RAYS + w->capE + 1) * NS * CTR_STRIDE * sizeof(unsigned), c->stream));
     // gen -> ray queue of bounce 0
     p.qo_out = w->qo[0]; p.qd_out = w->qd[0]; p.qid_out = w->qid[0];

@@ -110,7 +110,7 @@ typedef struct bdpt_params {
   int32_t samples_per_lane;   /* 0 = auto                                                 */
   int32_t device;             /* HIP device ordinal                                       */
   int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
-  int32_t pipeline;           /* 0 = wavefront (default), 1 = megakernel; same results    */
+  int32_t pipeline;           /* 0 = auto, 1 = megakernel, 2 = wavefront; same results     */
   int32_t reserved[4];
 } bdpt_params;
 
@@ -176,6 +176,17 @@ int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, fl
 /* Diagnostic hook: raw device counters (8 stats words + 8 phase-cycle words of a
  * BDPT_PHASE_PROF build). Sync. */
 int bdpt_debug_counters(void* ctx, uint64_t* out16);
+
+/* Host-side COLLADA loader: the reference CLI's scene path (ColladaParser::load,
+ * collada.cpp:129-941, + Application::load, application.cpp:228-304). width/height > 0 apply
+ * Camera::set_screen_size (-r W H). The desc returned by bdpt_dae_get_desc points into the
+ * loaded scene and stays valid until bdpt_dae_free. No device is touched. */
+typedef struct bdpt_dae bdpt_dae;
+int bdpt_dae_load(const char* path, int32_t width, int32_t height, bdpt_dae** out);
+int bdpt_dae_get_desc(const bdpt_dae* scene, bdpt_scene_desc* out);
+/* Writes the scene in the JSON dump format of tests/golden/scenes (round-trip doubles). */
+int bdpt_dae_dump_json(const bdpt_dae* scene, const char* path);
+void bdpt_dae_free(bdpt_dae* scene);
 
 #ifdef __cplusplus
 }

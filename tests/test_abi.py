@@ -1,0 +1,64 @@
+"""C-ABI boundary checks that need no GPU: libbdpt_amd.so loads and exports every function
+include/bdpt/bdpt.h declares; argument and scene validation happen before any device call."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import bdpt_amd as B
+from _util import REPO, golden_scene
+
+HEADER = os.path.join(REPO, "include", "bdpt", "bdpt.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(bdpt_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_declared_function():
+    names = declared_functions()
+    assert len(names) >= 18
+    lib = B.load_library()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", B.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (bdpt_\w+)", out))
+    assert set(names) <= exported, sorted(set(names) - exported)
+
+
+def test_abi_version():
+    assert B.load_library().bdpt_abi_version() == 1
+
+
+def test_null_arguments_rejected():
+    lib = B.load_library()
+    assert lib.bdpt_create(None, None, None) == -1
+    assert b"null" in lib.bdpt_last_error()
+
+
+def test_unsupported_material_rejected_before_device():
+    sc = golden_scene("CBspheres", 32, 24)
+    sc.mats[0].type = 5   # BDPT_MAT_MICROFACET: its sample_pdf asserts under BDPT (advanced_bsdf.cpp:144-148)
+    p = B.Params()
+    p.width, p.height, p.spp, p.max_depth = 32, 24, 1, 5
+    ctx = C.c_void_p()
+    lib = B.load_library()
+    assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) == -2
+    assert not ctx.value
+
+
+def test_bad_frame_size_rejected():
+    sc = golden_scene("CBspheres", 32, 24)
+    p = B.Params()
+    p.width, p.height, p.spp, p.max_depth = 0, 24, 1, 5
+    ctx = C.c_void_p()
+    assert B.load_library().bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) == -1
+
+
+def test_dae_missing_file():
+    with pytest.raises(Exception):
+        B.load_dae(os.path.join(REPO, "scenes", "no_such_scene.dae"))

@@ -17,11 +17,13 @@ from _util import MODE_C32, golden_scene, oracle, oracle_render
 pytestmark = pytest.mark.gpu
 
 RMSE_TOL = 1e-4
+PIPES = [pytest.param(B.PIPELINE_MEGAKERNEL, id="mega"), pytest.param(B.PIPELINE_WAVEFRONT, id="wave")]
 
 
-def _gpu_render(sc, W, H, S, M, seed=5489, tiles=(), ranges=None, spl=0, stats=False):
+def _gpu_render(sc, W, H, S, M, seed=5489, tiles=(), ranges=None, spl=0, stats=False,
+                pipeline=B.PIPELINE_AUTO):
     pt = B.BidirectionalPathTracer(sc, W, H, S, M, seed=seed, samples_per_lane=spl,
-                                   collect_stats=stats)
+                                   collect_stats=stats, pipeline=pipeline)
     try:
         if ranges is None:
             ranges = [(0, S)]
@@ -40,6 +42,7 @@ def _rmse(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)))
 
 
+@pytest.mark.parametrize("pipe", PIPES)
 @pytest.mark.parametrize("name,W,H,S,M", [
     ("CBspheres_lambertian", 160, 120, 4, 5),
     ("CBspheres", 160, 120, 4, 5),
@@ -49,9 +52,9 @@ def _rmse(a, b):
     ("CBspheres", 96, 72, 2, 1),
     ("CBspheres", 96, 72, 1, 12),
 ])
-def test_parity_vs_oracle(name, W, H, S, M):
+def test_parity_vs_oracle(name, W, H, S, M, pipe):
     sc = golden_scene(name, W, H)
-    g = _gpu_render(sc, W, H, S, M)
+    g = _gpu_render(sc, W, H, S, M, pipeline=pipe)
     samp, eye, light, st = oracle_render(sc, W, H, S, M, MODE_C32)
     assert np.isfinite(g["sample"]).all()
     r = _rmse(g["sample"], samp)
@@ -62,32 +65,36 @@ def test_parity_vs_oracle(name, W, H, S, M):
     assert r < RMSE_TOL and re < RMSE_TOL and rl < RMSE_TOL
 
 
-def test_parity_c2_full_frame():
+@pytest.mark.parametrize("pipe", PIPES)
+def test_parity_c2_full_frame(pipe):
     """Config C2's frame (CBspheres 480x360, m=5) at 4 spp: full-size FOV (splats land anywhere)."""
     sc = golden_scene("CBspheres", 480, 360)
-    g = _gpu_render(sc, 480, 360, 4, 5)
+    g = _gpu_render(sc, 480, 360, 4, 5, pipeline=pipe)
     samp = oracle_render(sc, 480, 360, 4, 5, MODE_C32)[0]
     assert _rmse(g["sample"], samp) < RMSE_TOL
 
 
-def test_tiles_and_sample_ranges_compose():
+@pytest.mark.parametrize("pipe", PIPES)
+def test_tiles_and_sample_ranges_compose(pipe):
     """raytrace_tile over 32x32 tiles (raytraced_renderer.cpp:297-301) and split sample ranges give
     the same image as one full-frame launch (sample keys are global: (pixel, sample))."""
     W, H, S, M = 100, 70, 4, 5
     sc = golden_scene("CBspheres", W, H)
-    full = _gpu_render(sc, W, H, S, M)
+    full = _gpu_render(sc, W, H, S, M, pipeline=pipe)
     tiles = [(x, y, 32, 32) for y in range(0, H, 32) for x in range(0, W, 32)]
-    tiled = _gpu_render(sc, W, H, S, M, tiles=tiles, ranges=[(0, 1), (1, 3), (3, 4)], spl=1)
+    tiled = _gpu_render(sc, W, H, S, M, tiles=tiles, ranges=[(0, 1), (1, 3), (3, 4)], spl=1,
+                        pipeline=pipe)
     assert _rmse(full["sample"], tiled["sample"]) < 1e-6
 
 
-def test_stats_counters_match_oracle():
+@pytest.mark.parametrize("pipe", PIPES)
+def test_stats_counters_match_oracle(pipe):
     """In-kernel counters (roofline bytes) against the oracle's counts of the same traversal work:
     closest-hit queries and hits are identical; the device skips zero-contribution connection rays
     and culls boxes, so shadow rays / node visits are <= the oracle's."""
     W, H, S, M = 64, 48, 2, 5
     sc = golden_scene("CBspheres", W, H)
-    g = _gpu_render(sc, W, H, S, M, stats=True)
+    g = _gpu_render(sc, W, H, S, M, stats=True, pipeline=pipe)
     st = g["stats"]
     o = oracle_render(sc, W, H, S, M, MODE_C32)[3]
     assert st.samples == W * H * S
@@ -129,3 +136,13 @@ def test_unsupported_material_rejected():
     sc.mats[0].type = B.MAT_MICROFACET
     with pytest.raises(B.BDPTError):
         B.BidirectionalPathTracer(sc, 32, 24, 1, 5)
+
+
+def test_pipelines_agree():
+    """Megakernel and wavefront evaluate the same per-sample arithmetic: images agree up to the
+    order of fp32 frame additions."""
+    W, H, S, M = 128, 96, 4, 5
+    sc = golden_scene("CBgems", W, H)
+    a = _gpu_render(sc, W, H, S, M, pipeline=B.PIPELINE_MEGAKERNEL)
+    b = _gpu_render(sc, W, H, S, M, pipeline=B.PIPELINE_WAVEFRONT)
+    assert _rmse(a["sample"], b["sample"]) < 1e-6

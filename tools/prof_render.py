@@ -19,7 +19,7 @@ launches = int(sys.argv[6]) if len(sys.argv) > 6 else 2
 if os.environ.get("BDPT_LIB"):
     B.load_library(os.environ["BDPT_LIB"])
     B._lib = B.load_library(os.environ["BDPT_LIB"])
-sc = golden_scene(scene, W, H)
+sc = B.load_dae(scene, W, H) if scene.endswith(".dae") else golden_scene(scene, W, H)
 pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489,
                                collect_stats=os.environ.get("BDPT_STATS") == "1")
 if os.environ.get("BDPT_WARM", "1") == "1":   # code-object load + first-launch setup, untimed
