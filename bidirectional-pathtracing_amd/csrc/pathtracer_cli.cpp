@@ -1,0 +1,157 @@
+// pathtracer_cli.cpp — the reference's `pathtracer` command line (src/application/main.cpp:62-200)
+// in windowless mode, rendering through libbdpt_amd.so on MI355X GPUs.
+//
+//   pathtracer [-s spp] [-m max_depth] [-r W H] [-f out.png] [-p x y dx dy] [-t threads]
+//              [-l n] [-g gpus] [-S seed] [--dump-scene scene.json] scene.dae
+//
+// Same flags and defaults as the reference (-s 1, -m 1, 800x600 when -r is absent; -t / -l are
+// accepted and do not apply to the GPU path; -p renders one cell). -g N splits the sample range
+// over N devices (one context and one host thread per device) and sums the frames.
+// Output: the tonemapped PNG and the "_rate.png" sampling-rate image, as render_to_file writes
+// them (raytraced_renderer.cpp:330-347, 690-761).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bdpt/bdpt.h"
+#include "image_io.h"
+
+namespace {
+
+void usage(const char* b) {
+  printf("Usage: %s [options] <scenefile>\n", b);
+  printf("Program Options:\n");
+  printf("  -s  <INT>        Number of camera rays per pixel\n");
+  printf("  -l  <INT>        Number of samples per area light (unused by BDPT)\n");
+  printf("  -t  <INT>        Number of render threads (GPU path: ignored)\n");
+  printf("  -m  <INT>        Maximum ray depth\n");
+  printf("  -f  <FILENAME>   Image (.png) file to save output to\n");
+  printf("  -r  <INT> <INT>  Width and height of output image\n");
+  printf("  -p  <x> <y> <dx> <dy>  Render only this cell\n");
+  printf("  -g  <INT>        Number of GPUs (default 1)\n");
+  printf("  -S  <INT>        RNG seed (default 5489)\n");
+  printf("  --dump-scene <FILE>  Write the loaded scene as JSON\n");
+  printf("  --tonemap <in.f64> <W> <H> <out.png>  Output stage only: raw float64 RGB (row 0 =\n"
+         "                   bottom) -> PNG + _rate.png, as render_to_file writes them\n");
+  printf("  -h               Print this help message\n");
+}
+
+int fail(const char* what) {
+  fprintf(stderr, "[PathTracer] %s: %s\n", what, bdpt_last_error());
+  return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int spp = 1, max_depth = 1, w = 0, h = 0, gpus = 1;
+  long cx = -1, cy = 0, cdx = 0, cdy = 0;
+  unsigned long long seed = 5489;
+  std::string out, dump, scene;
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    auto need = [&](int n) {
+      if (i + n >= argc) { usage(argv[0]); exit(1); }
+    };
+    if (a == "-s") { need(1); spp = atoi(argv[++i]); }
+    else if (a == "-m") { need(1); max_depth = atoi(argv[++i]); }
+    else if (a == "-t" || a == "-l") { need(1); ++i; }
+    else if (a == "-f") { need(1); out = argv[++i]; }
+    else if (a == "-r") { need(2); w = atoi(argv[i + 1]); h = atoi(argv[i + 2]); i += 2; }
+    else if (a == "-p") { need(4); cx = atol(argv[i + 1]); cy = atol(argv[i + 2]); cdx = atol(argv[i + 3]); cdy = atol(argv[i + 4]); i += 4; }
+    else if (a == "-g") { need(1); gpus = atoi(argv[++i]); }
+    else if (a == "-S") { need(1); seed = strtoull(argv[++i], nullptr, 10); }
+    else if (a == "--dump-scene") { need(1); dump = argv[++i]; }
+    else if (a == "--tonemap") {
+      need(4);
+      const int tw = atoi(argv[i + 2]), tht = atoi(argv[i + 3]);
+      std::vector<double> hdr((size_t)tw * tht * 3);
+      FILE* f = fopen(argv[i + 1], "rb");
+      if (!f || fread(hdr.data(), sizeof(double), hdr.size(), f) != hdr.size()) {
+        fprintf(stderr, "[PathTracer] cannot read %s\n", argv[i + 1]);
+        return 1;
+      }
+      fclose(f);
+      const std::string o = argv[i + 4];
+      if (!bdpt::write_png(o, bdpt::tonemap(hdr.data(), tw, tht), tw, tht)) return 1;
+      return bdpt::write_rate_png(o, std::vector<float>((size_t)tw * tht, 1.0f), tw, tht) ? 0 : 1;
+    }
+    else if (a == "-e" || a == "-c" || a == "-b" || a == "-d") {
+      fprintf(stderr, "[PathTracer] option %s is not supported by the BDPT GPU path\n", a.c_str());
+      return 1;
+    } else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
+    else scene = a;
+  }
+  if (scene.empty()) { usage(argv[0]); return 1; }
+  fprintf(stderr, "[PathTracer] Input scene file: %s\n", scene.c_str());
+  bdpt_dae* dae = nullptr;
+  if (bdpt_dae_load(scene.c_str(), w, h, &dae) != BDPT_OK) return fail("loading scene");
+  if (!dump.empty() && bdpt_dae_dump_json(dae, dump.c_str()) != BDPT_OK) return fail("dumping scene");
+  if (out.empty() && dump.empty()) {
+    fprintf(stderr, "[PathTracer] no -f: the interactive viewer is not part of this build\n");
+    return 1;
+  }
+  if (out.empty()) return 0;
+  if (w <= 0 || h <= 0) { w = 800; h = 600; }
+  bdpt_scene_desc desc;
+  bdpt_dae_get_desc(dae, &desc);
+  fprintf(stderr, "[PathTracer] %d primitives, %d materials, %d lights; %dx%d, %d spp, max depth %d, %d GPU(s)\n",
+          desc.nprim, desc.nmat, desc.nlight, w, h, spp, max_depth, gpus);
+
+  std::vector<bdpt_tile> tiles;
+  if (cx >= 0) tiles.push_back(bdpt_tile{(int32_t)cx, (int32_t)cy, (int32_t)cdx, (int32_t)cdy});
+  std::vector<std::vector<float>> frames(gpus, std::vector<float>((size_t)w * h * 3, 0.0f));
+  std::vector<int> rcs(gpus, 0);
+  std::vector<std::string> errs(gpus);
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int g = 0; g < gpus; g++) {
+    th.emplace_back([&, g] {
+      bdpt_params p;
+      memset(&p, 0, sizeof p);
+      p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed; p.device = g;
+      void* ctx = nullptr;
+      const int s0 = (int)((long long)spp * g / gpus), s1 = (int)((long long)spp * (g + 1) / gpus);
+      int rc = bdpt_create(&desc, &p, &ctx);
+      if (rc == BDPT_OK && s1 > s0)
+        rc = bdpt_render(ctx, tiles.empty() ? nullptr : tiles.data(), (int32_t)tiles.size(), s0, s1 - s0);
+      if (rc == BDPT_OK) rc = bdpt_read_frame(ctx, BDPT_FRAME_SAMPLE, frames[g].data());
+      if (rc != BDPT_OK) errs[g] = bdpt_last_error();
+      if (ctx) bdpt_destroy(ctx);
+      rcs[g] = rc;
+    });
+  }
+  for (auto& t : th) t.join();
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (int g = 0; g < gpus; g++)
+    if (rcs[g] != BDPT_OK) {
+      fprintf(stderr, "[PathTracer] GPU %d: %s\n", g, errs[g].c_str());
+      bdpt_dae_free(dae);
+      return 1;
+    }
+  std::vector<float>& img = frames[0];
+  for (int g = 1; g < gpus; g++)
+    for (size_t k = 0; k < img.size(); k++) img[k] += frames[g][k];
+  const double samples = (double)(tiles.empty() ? (long long)w * h : cdx * cdy) * spp;
+  fprintf(stderr, "[PathTracer] Rendering... 100%%! (%.4fs, %.2f Msamples/s)\n", secs, samples / secs / 1e6);
+  const std::vector<double> hdr(img.begin(), img.end());
+  const std::vector<uint32_t> rgba = bdpt::tonemap(hdr.data(), w, h);
+  fprintf(stderr, "[PathTracer] Saving to file: %s... ", out.c_str());
+  if (!bdpt::write_png(out, rgba, w, h)) { fprintf(stderr, "failed\n"); return 1; }
+  fprintf(stderr, "Done!\n");
+  std::vector<float> rate((size_t)w * h, 0.0f);
+  if (tiles.empty()) {
+    std::fill(rate.begin(), rate.end(), 1.0f);   // every pixel got ns_aa samples (bidirection.cpp:539)
+  } else {
+    for (long y = std::max(0L, cy); y < std::min((long)h, cy + cdy); y++)
+      for (long x = std::max(0L, cx); x < std::min((long)w, cx + cdx); x++) rate[(size_t)y * w + x] = 1.0f;
+  }
+  bdpt::write_rate_png(out, rate, w, h);
+  fprintf(stdout, "[PathTracer] Job completed.\n");
+  bdpt_dae_free(dae);
+  return 0;
+}
