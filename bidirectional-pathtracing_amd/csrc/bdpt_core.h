@@ -219,7 +219,8 @@ struct Counters {
 
 struct Hit {
   float t;
-  int prim;   // DFS position, -1 = none
+  int prim;   // position in the device tree's leaf order, -1 = none
+  int key;    // position in the reference tree's DFS leaf order (tie-break)
   float b1, b2;
 };
 
@@ -394,6 +395,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   RayInv r = make_rayinv(o, d);
   h.t = tmax;
   h.prim = -1;
+  h.key = -1;
   h.b1 = 0; h.b2 = 0;
   int stack_mem[BDPT_STACK];
   TravStack<K> stk(stack_mem);
@@ -407,15 +409,21 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       const int pi = st + k;
       float t, b1 = 0, b2 = 0;
       bool ok;
+      int key;
       if ((sm >> k) & 1) {
         c.sphs++;
         ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
+        key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
       } else {
         c.tris++;
-        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, h.t, &t, &b1, &b2);
+        const float4 g2 = GEOM[3 * pi + 2];
+        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
+        key = __float_as_int(g2.y);
       }
-      if (ok && (t < h.t || pi > h.prim)) {   // t <= h.t here: t == h.t only replaces a lower DFS index
-        h.t = t; h.prim = pi; h.b1 = b1; h.b2 = b2;
+      // t <= h.t here; an equal t replaces the hit only if it comes later in the reference's DFS
+      // leaf order (the reference keeps the last of equal-t hits)
+      if (ok && (t < h.t || key > h.key)) {
+        h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
       }
     }
     if (!stk.pop(ref)) break;
@@ -613,55 +621,6 @@ struct SampleParams {
   int W, H, spp, max_depth;
   uint64_t seed;
 };
-
-// Subpath random walk (prepare_bidirectional_subpath, bidirection.cpp:20-102). Vertex k of the
-// reference path is written to out[k - 2]; bit k of *dmask marks delta BSDFs.
-template <int MAXV, int LM = 0>
-BDPT_HD int random_walk(const SceneView& S, Rng& g, Counters& cnt, f3 o, f3 d, float tmin, float tmax,
-                        float point_pdf, float dir_pdf, f3 init_rad, f3 init_n, int max_depth, Vtx* out,
-                        uint32_t* dmask) {
-  f3 prev_alpha = divs(init_rad, point_pdf);
-  float prev_pdf = dir_pdf;
-  f3 prev_f = splat3(1.0f), prev_n = init_n;
-  int i = 2, count = 0;
-  uint32_t dm = 0;
-  f3 ro = o, rd = d;
-  float rmin = tmin, rmax = tmax;
-  for (;;) {
-    Hit h;
-    if (!trace_closest<LM>(S, ro, rd, rmin, rmax, h, cnt)) break;
-    f3 n;
-    int mat;
-    shade_hit(S, h, ro, rd, &n, &mat);
-    const DMat M = S.mats[mat];
-    Frame fr = make_frame(n);
-    f3 hit_p = add(ro, muls(rd, h.t));
-    f3 w_out = to_local(fr, neg(rd));
-    f3 wi;
-    float pdf;
-    f3 fv = sample_f(M, g, w_out, &wi, &pdf);
-    f3 wi_world = normalize(to_world(fr, wi));
-    float cp = dot(prev_n, rd);
-    Vtx v;
-    v.alpha = divs(mul(muls(prev_alpha, fabsf(cp)), prev_f), prev_pdf);
-    v.pos = hit_p;
-    v.n = n;
-    v.zh = fr.Z;
-    v.mat = mat;
-    v.fwd = 1; v.gp = 0; v.conn = 0;
-    out[count++] = v;
-    if (is_delta(M.type)) dm |= 1u << i;
-    if (i >= max_depth + 1 || count >= MAXV) break;
-    ro = hit_p; rd = wi_world; rmin = BDPT_EPS_F; rmax = INFINITY;
-    prev_f = fv;
-    prev_n = n;
-    prev_pdf = pdf * 1.0f;
-    prev_alpha = v.alpha;
-    i++;
-  }
-  *dmask = dm;
-  return count;
-}
 
 // Power-heuristic sums in Horner form. Along a subpath walked from the connection endpoint
 // inward, the reference accumulates ratio_k = f_end * ... * f_k and adds ratio_k^2 when neither
@@ -917,7 +876,11 @@ struct PathsInRegs {
 };
 
 // Eye and light subpaths of one pixel-sample plus their MIS constants
-// (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524).
+// (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524;
+// prepare_bidirectional_subpath :20-102 for both walks). The two walks run as ONE loop: a lane whose
+// eye walk ends starts its light walk in the next iteration, so a wave iterates
+// max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
+// sample + walk: 1) make the interleaving invisible in the results.
 template <int MAXV, int LM = 0>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
@@ -929,43 +892,46 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   float dx = px / (float)sp.W, dy = py / (float)sp.H;
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   f3 rd = camera_dir(S.cam, dx, dy);
-  int ne = random_walk<MAXV, LM>(S, g, cnt, cam, rd, S.cam.nclip, S.cam.fclip, 1.0f, 1.0f, splat3(1.0f), rd,
-                             sp.max_depth, P.E, &P.dE);
-  P.nE = ne + 2;
-  // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le
-  rng_stream(g, 1);
-  int lid = (int)(rng_next(g) * (float)S.nlights);
-  if (lid >= S.nlights) lid = S.nlights - 1;
-  const DLight& L0 = S.lights[lid];
+  // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le, on stream 1
   f3 lo, ld, ln;
   float lpp, ldp;
-  f3 lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
-  if (L0.type == LIGHT_POINT) {
-    float z = rng_next(g) * 2 - 1;
-    float sinT = sqrtf(fmaxf(0.0f, 1.0f - z * z));
-    float u = rng_next(g);
-    float c, s;
-    cos_sin_2pi(u, &c, &s);
-    ld = mk3(c * sinT, s * sinT, z);
-    lo = mk3(L0.pos[0], L0.pos[1], L0.pos[2]);
-    lpp = 1;
-    ldp = 0.25f / BDPT_PI_F;
-    ln = ld;
-  } else {
-    float sx, sy;
-    grid2d(g, &sx, &sy);
-    sx = sx - 0.5f;
-    sy = sy - 0.5f;
-    lo = add(add(mk3(L0.pos[0], L0.pos[1], L0.pos[2]), smul(sx, mk3(L0.dx[0], L0.dx[1], L0.dx[2]))),
-             smul(sy, mk3(L0.dy[0], L0.dy[1], L0.dy[2])));
-    f3 dl = cosine_hemi(g, &ldp);
-    Frame lf;
-    lf.X = mk3(L0.fx[0], L0.fx[1], L0.fx[2]);
-    lf.Y = mk3(L0.fy[0], L0.fy[1], L0.fy[2]);
-    lf.Z = mk3(L0.fz[0], L0.fz[1], L0.fz[2]);
-    ld = to_world(lf, dl);
-    lpp = 1.0f / L0.area;
-    ln = mk3(L0.dir[0], L0.dir[1], L0.dir[2]);
+  f3 lrad;
+  uint32_t lpos;
+  {
+    Rng gl = g;
+    rng_stream(gl, 1);
+    int lid = (int)(rng_next(gl) * (float)S.nlights);
+    if (lid >= S.nlights) lid = S.nlights - 1;
+    const DLight& L0 = S.lights[lid];
+    lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
+    if (L0.type == LIGHT_POINT) {
+      float z = rng_next(gl) * 2 - 1;
+      float sinT = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+      float u = rng_next(gl);
+      float c, s;
+      cos_sin_2pi(u, &c, &s);
+      ld = mk3(c * sinT, s * sinT, z);
+      lo = mk3(L0.pos[0], L0.pos[1], L0.pos[2]);
+      lpp = 1;
+      ldp = 0.25f / BDPT_PI_F;
+      ln = ld;
+    } else {
+      float sx, sy;
+      grid2d(gl, &sx, &sy);
+      sx = sx - 0.5f;
+      sy = sy - 0.5f;
+      lo = add(add(mk3(L0.pos[0], L0.pos[1], L0.pos[2]), smul(sx, mk3(L0.dx[0], L0.dx[1], L0.dx[2]))),
+               smul(sy, mk3(L0.dy[0], L0.dy[1], L0.dy[2])));
+      f3 dl = cosine_hemi(gl, &ldp);
+      Frame lf;
+      lf.X = mk3(L0.fx[0], L0.fx[1], L0.fx[2]);
+      lf.Y = mk3(L0.fy[0], L0.fy[1], L0.fy[2]);
+      lf.Z = mk3(L0.fz[0], L0.fz[1], L0.fz[2]);
+      ld = to_world(lf, dl);
+      lpp = 1.0f / L0.area;
+      ln = mk3(L0.dir[0], L0.dir[1], L0.dir[2]);
+    }
+    lpos = gl.pos;
   }
   lpp = lpp / (float)S.nlights;
   {
@@ -978,10 +944,70 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.gp = 0; v1.conn = 0;
   }
   P.l1_dir_pdf = ldp;
-  uint32_t dl = 0;
-  int nl = random_walk<MAXV, LM>(S, g, cnt, lo, ld, BDPT_EPS_F, INFINITY, lpp, ldp, lrad, ln, sp.max_depth, P.L + 1, &dl);
-  P.dL = dl;
-  P.nL = nl + 2;
+  // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
+  f3 ro = cam;
+  float rmin = S.cam.nclip, rmax = S.cam.fclip;
+  f3 prev_alpha = divs(splat3(1.0f), 1.0f);
+  float prev_pdf = 1.0f;
+  f3 prev_f = splat3(1.0f), prev_n = rd;
+  int i = 2, count = 0;
+  uint32_t dm = 0;
+  bool light = false;
+  for (;;) {
+    Hit h;
+    bool end = !trace_closest<LM>(S, ro, rd, rmin, rmax, h, cnt);
+    if (!end) {
+      f3 n;
+      int mat;
+      shade_hit(S, h, ro, rd, &n, &mat);
+      const DMat M = S.mats[mat];
+      const Frame fr = make_frame(n);
+      const f3 hit_p = add(ro, muls(rd, h.t));
+      Vtx v;
+      v.alpha = divs(mul(muls(prev_alpha, fabsf(dot(prev_n, rd))), prev_f), prev_pdf);
+      v.pos = hit_p;
+      v.n = n;
+      v.zh = fr.Z;
+      v.mat = mat;
+      v.fwd = 1; v.gp = 0; v.conn = 0;
+      (light ? P.L + 1 : P.E)[count++] = v;
+      if (is_delta(M.type)) dm |= 1u << i;
+      if (i >= sp.max_depth + 1 || count >= MAXV) {
+        end = true;
+      } else {
+        f3 wi;
+        float pdf;
+        const f3 fv = sample_f(M, g, to_local(fr, neg(rd)), &wi, &pdf);
+        ro = hit_p;
+        rd = normalize(to_world(fr, wi));
+        rmin = BDPT_EPS_F;
+        rmax = INFINITY;
+        prev_f = fv;
+        prev_n = n;
+        prev_pdf = pdf * 1.0f;
+        prev_alpha = v.alpha;
+        i++;
+      }
+    }
+    if (end) {
+      if (light) {
+        P.nL = count + 2;
+        P.dL = dm;
+        break;
+      }
+      P.nE = count + 2;
+      P.dE = dm;
+      light = true;
+      rng_stream(g, 1);
+      g.pos = lpos;
+      ro = lo; rd = ld; rmin = BDPT_EPS_F; rmax = INFINITY;
+      prev_alpha = divs(lrad, lpp);
+      prev_pdf = ldp;
+      prev_f = splat3(1.0f);
+      prev_n = ln;
+      i = 2; count = 0; dm = 0;
+    }
+  }
   eye_constants<MAXV>(S, P);
   light_constants<MAXV>(S, P, lpp);
 }

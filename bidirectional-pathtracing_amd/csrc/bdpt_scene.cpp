@@ -3,7 +3,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 namespace bdpt {
 
@@ -91,6 +93,101 @@ struct Builder {
     nodes.push_back(Node());
     int l = build(left, d + 1);
     int r = build(right, d + 1);
+    Box bb = nodes[l].box;
+    bb.expand(nodes[r].box);
+    nodes[id].l = l;
+    nodes[id].r = r;
+    nodes[id].box = bb;
+    return id;
+  }
+};
+
+// Device tree: binned SAH (16 bins per axis on centroid bounds, leaves of <= 4 primitives as the
+// leaf encoding requires). Which tree the device traverses does not change any result: closest
+// hits are decided by t, ties by the primitive's position in the REFERENCE tree's DFS leaf order
+// (the reference keeps the last of equal-t hits, bvh.cpp:161-188), and any-hit is order free.
+struct SahBuilder {
+  const std::vector<Box>* pb;
+  std::vector<Node> nodes;
+  std::vector<int> leaf_prims;
+  int depth = 0;
+  static double area(const Box& b) {
+    const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+    return dx < 0 ? 0 : 2 * (dx * dy + dy * dz + dz * dx);
+  }
+  int make_leaf(const int* prims, int n) {
+    Node nd;
+    nd.box = (*pb)[prims[0]];
+    for (int k = 0; k < n; k++) nd.box.expand((*pb)[prims[k]]);
+    nd.start = (int)leaf_prims.size();
+    nd.count = n;
+    for (int k = 0; k < n; k++) leaf_prims.push_back(prims[k]);
+    nodes.push_back(nd);
+    return (int)nodes.size() - 1;
+  }
+  int build(int* prims, int n, int d) {
+    depth = std::max(depth, d);
+    const auto& B = *pb;
+    if (n <= 4) return make_leaf(prims, n);
+    Box cb;
+    for (int k = 0; k < 3; k++) { cb.mn[k] = INFINITY; cb.mx[k] = -INFINITY; }
+    for (int i = 0; i < n; i++) {
+      double c[3] = {B[prims[i]].centroid(0), B[prims[i]].centroid(1), B[prims[i]].centroid(2)};
+      cb.expand_pt(c);
+    }
+    constexpr int NB = 16;
+    double best = INFINITY;
+    int best_axis = -1, best_split = 0;
+    for (int ax = 0; ax < 3; ax++) {
+      const double lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
+      if (!(ext > 0)) continue;
+      Box bb[NB];
+      int cnt[NB] = {0};
+      for (int b = 0; b < NB; b++)
+        for (int k = 0; k < 3; k++) { bb[b].mn[k] = INFINITY; bb[b].mx[k] = -INFINITY; }
+      for (int i = 0; i < n; i++) {
+        int b = (int)((B[prims[i]].centroid(ax) - lo) / ext * NB);
+        b = std::min(NB - 1, std::max(0, b));
+        cnt[b]++;
+        bb[b].expand(B[prims[i]]);
+      }
+      double ra[NB];
+      int rc[NB];
+      Box acc;
+      for (int k = 0; k < 3; k++) { acc.mn[k] = INFINITY; acc.mx[k] = -INFINITY; }
+      int c = 0;
+      for (int b = NB - 1; b > 0; b--) {
+        acc.expand(bb[b]);
+        c += cnt[b];
+        ra[b] = area(acc);
+        rc[b] = c;
+      }
+      for (int k = 0; k < 3; k++) { acc.mn[k] = INFINITY; acc.mx[k] = -INFINITY; }
+      c = 0;
+      for (int b = 0; b < NB - 1; b++) {
+        acc.expand(bb[b]);
+        c += cnt[b];
+        if (c == 0 || rc[b + 1] == 0) continue;
+        const double cost = area(acc) * c + ra[b + 1] * rc[b + 1];
+        if (cost < best) { best = cost; best_axis = ax; best_split = b + 1; }
+      }
+    }
+    int nl;
+    if (best_axis < 0) {
+      nl = n / 2;   // coincident centroids: split in input order
+    } else {
+      const double lo = cb.mn[best_axis], ext = cb.mx[best_axis] - cb.mn[best_axis];
+      int* mid = std::stable_partition(prims, prims + n, [&](int p) {
+        int b = (int)((B[p].centroid(best_axis) - lo) / ext * NB);
+        return std::min(NB - 1, std::max(0, b)) < best_split;
+      });
+      nl = (int)(mid - prims);
+      if (nl == 0 || nl == n) nl = n / 2;
+    }
+    const int id = (int)nodes.size();
+    nodes.push_back(Node());
+    const int l = build(prims, nl, d + 1);
+    const int r = build(prims + nl, n - nl, d + 1);
     Box bb = nodes[l].box;
     bb.expand(nodes[r].box);
     nodes[id].l = l;
@@ -197,22 +294,44 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
       return BDPT_E_INVALID;
     }
   }
-  Builder B;
-  B.pb = &pb;
+  // the reference's tree: its DFS leaf order is the tie-break key of every primitive
+  Builder R;
+  R.pb = &pb;
   std::vector<int> all(n);
   for (int i = 0; i < n; i++) all[i] = i;
-  int root = B.build(all, 0);
-  out.depth = B.depth;
-  out.ref_nodes = (int)B.nodes.size();
+  const int ref_root = R.build(all, 0);
+  out.depth = R.depth;
+  out.ref_nodes = (int)R.nodes.size();
   out.nprim = n;
-  if (out.depth + 2 > BDPT_STACK) { err = "BVH deeper than the traversal stack"; return BDPT_E_UNSUPPORTED; }
+  out.ref_order = R.leaf_prims;
+  std::vector<int> ref_pos(n);
+  for (int k = 0; k < n; k++) ref_pos[R.leaf_prims[k]] = k;
+  // the device's tree (BDPT_BVH=ref traverses the reference's own tree instead)
+  const char* bvh_env = getenv("BDPT_BVH");
+  const bool use_ref = bvh_env && std::string(bvh_env) == "ref";
+  Builder Bs;
+  int root = ref_root;
+  if (!use_ref) {
+    SahBuilder S;
+    S.pb = &pb;
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; i++) idx[i] = i;
+    root = S.build(idx.data(), n, 0);
+    Bs.nodes = std::move(S.nodes);
+    Bs.leaf_prims = std::move(S.leaf_prims);
+    Bs.depth = S.depth;
+  }
+  Builder& T = use_ref ? R : Bs;
+  out.dev_depth = T.depth;
+  out.dev_nodes = (int)T.nodes.size();
+  if (T.depth + 2 > BDPT_STACK) { err = "BVH deeper than the traversal stack"; return BDPT_E_UNSUPPORTED; }
 
-  // primitives in DFS leaf order
-  out.prim_ref = B.leaf_prims;
+  // primitives in the device tree's DFS leaf order
+  out.prim_ref = T.leaf_prims;
   out.geom.assign(12 * (size_t)n, 0.0f);
   out.shade.assign(12 * (size_t)n, 0.0f);
   for (int k = 0; k < n; k++) {
-    int i = B.leaf_prims[k];
+    int i = T.leaf_prims[k];
     const double* g = d->prim_geom + 18 * (size_t)i;
     float* G = &out.geom[12 * (size_t)k];
     float* S = &out.shade[12 * (size_t)k];
@@ -224,27 +343,29 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
       G[0] = p1[0]; G[1] = p1[1]; G[2] = p1[2]; G[3] = e1[0];
       G[4] = e1[1]; G[5] = e1[2]; G[6] = e2[0]; G[7] = e2[1];
       G[8] = e2[2];
+      G[9] = i2f(ref_pos[i]);   // tie-break key (third float4 .y)
       for (int c3 = 0; c3 < 9; c3++) S[c3] = (float)g[9 + c3];
       S[9] = i2f(d->prim_mat[i]);
       S[10] = i2f(0);
     } else {
       G[0] = (float)g[0]; G[1] = (float)g[1]; G[2] = (float)g[2]; G[3] = (float)g[3];
+      G[4] = i2f(ref_pos[i]);   // tie-break key (second float4 .x)
       S[9] = i2f(d->prim_mat[i]);
       S[10] = i2f(1);
     }
   }
   // nodes: the top kTopNodes internal nodes in BFS order (the LDS treelet: every ray starts
   // there), then the rest in DFS pre-order (subtrees contiguous for the global fetches).
-  std::vector<int> dev_index(B.nodes.size(), -1);
+  std::vector<int> dev_index(T.nodes.size(), -1);
   std::vector<int> order;
-  if (B.nodes[root].l >= 0) {
+  if (T.nodes[root].l >= 0) {
     std::vector<int> bfs{root};
     for (size_t h = 0; h < bfs.size() && (int)order.size() < kTopNodes; h++) {
       int id = bfs[h];
       dev_index[id] = (int)order.size();
       order.push_back(id);
-      for (int ch : {B.nodes[id].l, B.nodes[id].r})
-        if (B.nodes[ch].l >= 0) bfs.push_back(ch);
+      for (int ch : {T.nodes[id].l, T.nodes[id].r})
+        if (T.nodes[ch].l >= 0) bfs.push_back(ch);
     }
     out.n_top = (int)order.size();
     std::vector<int> st{root};
@@ -255,16 +376,16 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
         dev_index[id] = (int)order.size();
         order.push_back(id);
       }
-      if (B.nodes[B.nodes[id].r].l >= 0) st.push_back(B.nodes[id].r);
-      if (B.nodes[B.nodes[id].l].l >= 0) st.push_back(B.nodes[id].l);
+      if (T.nodes[T.nodes[id].r].l >= 0) st.push_back(T.nodes[id].r);
+      if (T.nodes[T.nodes[id].l].l >= 0) st.push_back(T.nodes[id].l);
     }
   }
   auto ref_of = [&](int id) -> int {
-    const Node& nd = B.nodes[id];
+    const Node& nd = T.nodes[id];
     if (nd.l >= 0) return dev_index[id];
     int mask = 0;
     for (int k = 0; k < nd.count; k++) {
-      int i = B.leaf_prims[nd.start + k];
+      int i = T.leaf_prims[nd.start + k];
       if (d->prim_type[i] == BDPT_PRIM_SPHERE) mask |= 1 << k;
     }
     uint32_t enc = ((uint32_t)nd.start << 7) | ((uint32_t)mask << 3) | (uint32_t)nd.count;
@@ -272,9 +393,9 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
   };
   out.nodes.assign(16 * order.size(), 0.0f);
   for (size_t k = 0; k < order.size(); k++) {
-    const Node& nd = B.nodes[order[k]];
+    const Node& nd = T.nodes[order[k]];
     float* N = &out.nodes[16 * k];
-    const Box* cb[2] = {&B.nodes[nd.l].box, &B.nodes[nd.r].box};
+    const Box* cb[2] = {&T.nodes[nd.l].box, &T.nodes[nd.r].box};
     float v[12];
     for (int s = 0; s < 2; s++) {
       const Box& b = *cb[s];

@@ -25,13 +25,15 @@ struct HostScene {
   std::vector<float> nodes;   // 16 floats per node
   std::vector<float> geom;    // 12 floats per prim
   std::vector<float> shade;   // 12 floats per prim
-  std::vector<int32_t> prim_ref;
+  std::vector<int32_t> prim_ref;    // device DFS position -> scene primitive index
+  std::vector<int32_t> ref_order;   // the reference tree's DFS leaf order (scene indices)
   std::vector<DMat> mats;
   std::vector<DLight> lights;
   DCam cam;
   int root = 0;               // root child reference (node index or encoded leaf)
   int depth = 0;              // reference BVH depth (root = 0)
   int ref_nodes = 0;          // node count of the reference binary tree
+  int dev_nodes = 0, dev_depth = 0;   // the device tree (SAH by default)
   int nprim = 0;
   int n_top = 0;              // leading nodes in BFS order (LDS treelet candidates)
 };

@@ -78,6 +78,6 @@ extern "C" int core_cpu_scene_info(const bdpt_scene_desc* d, int* depth, int* re
   if (rc) return rc;
   *depth = hs.depth;
   *ref_nodes = hs.ref_nodes;
-  for (size_t i = 0; i < hs.prim_ref.size(); i++) prim_ref[i] = hs.prim_ref[i];
+  for (size_t i = 0; i < hs.ref_order.size(); i++) prim_ref[i] = hs.ref_order[i];
   return 0;
 }
