@@ -75,12 +75,14 @@ struct WfParams {
   float4* hits;           // (t, prim, b1, b2) per queue entry
   unsigned* cand;         // slot | i << 22 | j << 27
   float4 *so, *sd, *sv;   // shadow queue: (o, tmax) (d, target) (value)
+  unsigned char* svis;    // per shadow entry: 1 = unoccluded (refill traversal -> k_wf_resolve)
   unsigned* ctr;          // kMaxQueues counter blocks
   int cin, cout;          // counter blocks of the in / out ray queues
   unsigned cap_ray, cap_cand, cap_sh;   // entries per stripe
   int n_node4, n_geom4;
   float inv_spp;
   int point_light;        // scene has a point light: its t = 1, s = 1 splats all hit one pixel
+  unsigned lds_scene;     // bytes of LDS scene copy (the wave pools follow it)
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -602,6 +604,228 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_shadow(WfParams p) {
   if (STATS) flush_stats(p.stats, 0, cnt);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Traversal with lane refill (Aila & Laine 2009, "persistent while-while with dynamic fetch"): a
+// lane whose ray is finished takes the next queued ray instead of idling until the slowest lane
+// of its wave is done. Each wave owns a 128-entry LDS pool of queue indices, refilled chunk by
+// chunk (64 entries) from its static share of the striped queue; lanes advance one leaf visit
+// at a time and the wave refills while it is less than 3/4 busy.
+constexpr int kPool = 128;
+#ifndef BDPT_REFILL_BELOW
+#define BDPT_REFILL_BELOW 48
+#endif
+constexpr int kRefillBelow = BDPT_REFILL_BELOW;
+
+struct WavePool {
+  int* ids;
+  unsigned next;     // next chunk of this wave's static share (wave-uniform)
+  int head, count;   // wave-uniform
+  __device__ void refill(const QView& qv, unsigned nw) {
+    while (count < 64 && next < qv.total) {
+      unsigned r;
+      const bool v = qv.entry(next, r);
+      const unsigned long long m = __ballot(v);
+      if (v) ids[(head + count + lanes_below(m)) & (kPool - 1)] = (int)r;
+      count += __popcll(m);
+      next += nw;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // returns true for an idle lane that received entry *rid
+  __device__ bool assign(bool active, unsigned* rid) {
+    const unsigned long long idle = __ballot(!active);
+    const int take = min(__popcll(idle), count);
+    bool got = false;
+    if (!active) {
+      const int rank = lanes_below(idle);
+      if (rank < take) {
+        *rid = (unsigned)ids[(head + rank) & (kPool - 1)];
+        got = true;
+      }
+    }
+    head += take;
+    count -= take;
+    __builtin_amdgcn_wave_barrier();
+    return got;
+  }
+  __device__ bool more(const QView& qv) const { return count > 0 || next < qv.total; }
+};
+
+// one leaf visit of a closest-hit query: descend to a leaf, test it; true when finished
+template <int LM, int K>
+__device__ __forceinline__ bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
+                                             int& ref, TravStack<K>& stk, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
+  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
+  if (ref == kTravDone) return true;
+  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  for (int k = 0; k < cnt; k++) {
+    const int pi = st + k;
+    float t, b1 = 0, b2 = 0;
+    bool ok;
+    int key;
+    if ((sm >> k) & 1) {
+      c.sphs++;
+      ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
+      key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
+    } else {
+      c.tris++;
+      const float4 g2 = GEOM[3 * pi + 2];
+      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
+      key = __float_as_int(g2.y);
+    }
+    if (ok && (t < h.t || key > h.key)) {   // same rule as trace_closest (bdpt_core.h)
+      h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
+    }
+  }
+  return !stk.pop(ref);
+}
+
+// one leaf visit of an any-hit query: true when finished (*hit tells whether something was hit)
+template <int LM, int K>
+__device__ __forceinline__ bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
+                                         int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
+  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
+  if (ref == kTravDone) { *hit = false; return true; }
+  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  for (int k = 0; k < cnt; k++) {
+    const int pi = st + k;
+    float t, b1, b2;
+    bool ok;
+    if ((sm >> k) & 1) {
+      c.sphs++;
+      ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
+    } else {
+      c.tris++;
+      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+    }
+    if (ok) { *hit = true; return true; }
+  }
+  if (!stk.pop(ref)) { *hit = false; return true; }
+  return false;
+}
+
+template <int LM, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace_rf(WfParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  stage_scene<LM>(p, (float4*)smem);
+  QView qv;
+  qv.init(qctr(p, p.cin), p.cap_ray);
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  WavePool pool{(int*)(smem + p.lds_scene) + (threadIdx.x >> 6) * kPool, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, 0, 0};
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  bool active = false;
+  unsigned rid = 0;
+  f3 o = splat3(0), d = splat3(0);
+  float tmin = 0;
+  RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
+  Hit h;
+  h.t = 0; h.prim = -1; h.key = -1; h.b1 = 0; h.b2 = 0;
+  int ref = 0;
+  int stack_mem[BDPT_STACK];
+  TravStack<kRegStack> stk(stack_mem);
+  for (;;) {
+    pool.refill(qv, nw);
+    if (pool.assign(active, &rid)) {
+      const float4 a = p.qo_in[rid], b = p.qd_in[rid];
+      o = mk3(a.x, a.y, a.z);
+      d = mk3(b.x, b.y, b.z);
+      tmin = a.w;
+      r = make_rayinv(o, d);
+      h.t = b.w; h.prim = -1; h.key = -1; h.b1 = 0; h.b2 = 0;
+      ref = p.S.root;
+      stk.nreg = 0;
+      stk.msp = 0;
+      cnt.closest++;
+      active = true;
+    }
+    if (__ballot(active) == 0) break;
+    for (;;) {
+      if (active && closest_step<LM, kRegStack>(p.S, r, o, d, tmin, h, ref, stk, cnt)) {
+        if (h.prim >= 0) cnt.hits++;
+        p.hits[rid] = make_float4(h.t, __int_as_float(h.prim), h.b1, h.b2);
+        active = false;
+      }
+      const int na = __popcll(__ballot(active));
+      if (na == 0 || (na < kRefillBelow && pool.more(qv))) break;
+    }
+  }
+  if (STATS) flush_stats(p.stats, 0, cnt);
+}
+
+template <int LM, bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_shadow_rf(WfParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  stage_scene<LM>(p, (float4*)smem);
+  QView qv;
+  qv.init(qctr(p, Q_SHADOW), p.cap_sh);
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  WavePool pool{(int*)(smem + p.lds_scene) + (threadIdx.x >> 6) * kPool, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, 0, 0};
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  bool active = false;
+  unsigned rid = 0;
+  f3 o = splat3(0), d = splat3(0);
+  float tmax = 0;
+  RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
+  int ref = 0;
+  int stack_mem[BDPT_STACK];
+  TravStack<kRegStack> stk(stack_mem);
+  for (;;) {
+    pool.refill(qv, nw);
+    if (pool.assign(active, &rid)) {
+      const float4 a = p.so[rid], b = p.sd[rid];
+      o = mk3(a.x, a.y, a.z);
+      d = mk3(b.x, b.y, b.z);
+      tmax = a.w;
+      r = make_rayinv(o, d);
+      ref = p.S.root;
+      stk.nreg = 0;
+      stk.msp = 0;
+      cnt.shadow++;
+      active = true;
+    }
+    if (__ballot(active) == 0) break;
+    for (;;) {
+      bool hit = false;
+      if (active && any_step<LM, kRegStack>(p.S, r, o, d, BDPT_EPS_F, tmax, ref, stk, &hit, cnt)) {
+        p.svis[rid] = hit ? 0 : 1;   // resolved into the frames by k_wf_resolve
+        active = false;
+      }
+      const int na = __popcll(__ballot(active));
+      if (na == 0 || (na < kRefillBelow && pool.more(qv))) break;
+    }
+  }
+  if (STATS) flush_stats(p.stats, 0, cnt);
+}
+
+// Adds the unoccluded connection values to the frames, walking the shadow queue in its own order:
+// a slot's connection rays sit next to each other, so eye-image values reduce to one atomic per
+// run of equal pixels (seg_add) and point-light t=1 splats to one per wave (wave_add).
+__global__ __launch_bounds__(kBlock) void k_wf_resolve(WfParams p) {
+  QView qv;
+  qv.init(qctr(p, Q_SHADOW), p.cap_sh);
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  for (unsigned c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < qv.total; c += nw) {
+    unsigned r;
+    const bool valid = qv.entry(c, r);
+    const bool vis = valid && p.svis[r] != 0;
+    int tgt = 0;
+    bool hot = false;
+    f3 v = splat3(0);
+    if (vis) {
+      tgt = __float_as_int(p.sd[r].w);
+      const float4 w = p.sv[r];
+      v = mk3(w.x, w.y, w.z);
+      hot = w.w != 0.0f;
+    }
+    seg_add(p.eye, vis && tgt < 0, ~tgt, v);
+    wave_add(p.light, vis && tgt >= 0 && hot, tgt, v, 8);
+    wave_add(p.light, vis && tgt >= 0 && !hot, tgt, v, 1);
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -617,6 +841,7 @@ struct WfState {
   float4* hits = nullptr;
   unsigned* cand = nullptr;
   float4 *so = nullptr, *sd = nullptr, *sv = nullptr;
+  unsigned char* svis = nullptr;
   unsigned* ctr = nullptr;
   unsigned cap_ray = 0, cap_cand = 0, cap_sh = 0;   // entries per stripe
   int lm = -1, ntop = 0;
@@ -627,7 +852,7 @@ void wf_free(Ctx* c) {
   WfState* w = c->wf;
   if (!w) return;
   void* bufs[] = {w->vA, w->vB, w->vC, w->hdr, w->w0, w->w1, w->w2, w->w3, w->qo[0], w->qo[1], w->qd[0], w->qd[1],
-                  w->qid[0], w->qid[1], w->hits, w->cand, w->so, w->sd, w->sv, w->ctr};
+                  w->qid[0], w->qid[1], w->hits, w->cand, w->so, w->sd, w->sv, w->svis, w->ctr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete w;
@@ -669,7 +894,7 @@ int wf_alloc(Ctx* c) {
       (rc = dalloc(&w->qd[0], nray)) || (rc = dalloc(&w->qd[1], nray)) ||
       (rc = dalloc(&w->qid[0], nray)) || (rc = dalloc(&w->qid[1], nray)) ||
       (rc = dalloc(&w->hits, nray)) || (rc = dalloc(&w->cand, w->ncand)) || (rc = dalloc(&w->so, w->ncand)) ||
-      (rc = dalloc(&w->sd, w->ncand)) || (rc = dalloc(&w->sv, w->ncand)) ||
+      (rc = dalloc(&w->sd, w->ncand)) || (rc = dalloc(&w->sv, w->ncand)) || (rc = dalloc(&w->svis, w->ncand)) ||
       (rc = dalloc(&w->ctr, (size_t)kMaxQueues * NS * CTR_STRIDE))) {
     wf_free(c);
     return rc;
@@ -699,10 +924,32 @@ int launch(Ctx* c, K kernel, int block, size_t lds, const WfParams& p, long long
   return BDPT_OK;
 }
 
+// BDPT_WF_REFILL: bit 0 = refill traversal for walk rays (default on), bit 1 = refill traversal
+// for connection rays + separate k_wf_resolve (default off: the fused kernel overlaps its frame
+// atomics with traversal, which measured faster)
+int wf_refill_mask() {
+  static const int m = getenv("BDPT_WF_REFILL") ? atoi(getenv("BDPT_WF_REFILL")) : 1;
+  return m;
+}
+bool wf_refill() { return (wf_refill_mask() & 2) != 0; }
+
 template <bool STATS>
 int trace_launch(Ctx* c, WfParams& p, bool shadow, long long work) {
   WfState* w = c->wf;
   p.S.ntop = w->ntop;
+  p.lds_scene = (unsigned)((w->lds + 15) & ~(size_t)15);
+  const bool rf = shadow ? wf_refill() : (wf_refill_mask() & 1) != 0;
+  if (rf) {
+    const size_t lds = p.lds_scene + (size_t)(kTraceBlock / 64) * kPool * sizeof(int);
+    if (shadow) {
+      if (w->lm == 1) return launch(c, k_wf_shadow_rf<1, STATS>, kTraceBlock, lds, p, work);
+      if (w->lm == 2) return launch(c, k_wf_shadow_rf<2, STATS>, kTraceBlock, lds, p, work);
+      return launch(c, k_wf_shadow_rf<0, STATS>, kTraceBlock, lds, p, work);
+    }
+    if (w->lm == 1) return launch(c, k_wf_trace_rf<1, STATS>, kTraceBlock, lds, p, work);
+    if (w->lm == 2) return launch(c, k_wf_trace_rf<2, STATS>, kTraceBlock, lds, p, work);
+    return launch(c, k_wf_trace_rf<0, STATS>, kTraceBlock, lds, p, work);
+  }
   if (shadow) {
     if (w->lm == 1) return launch(c, k_wf_shadow<1, STATS>, kTraceBlock, w->lds, p, work);
     if (w->lm == 2) return launch(c, k_wf_shadow<2, STATS>, kTraceBlock, w->lds, p, work);
@@ -712,7 +959,6 @@ int trace_launch(Ctx* c, WfParams& p, bool shadow, long long work) {
   if (w->lm == 2) return launch(c, k_wf_trace<2, STATS>, kTraceBlock, w->lds, p, work);
   return launch(c, k_wf_trace<0, STATS>, kTraceBlock, 0, p, work);
 }
-
 
 }  // namespace
 
@@ -740,7 +986,7 @@ int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, i
   p.w0 = w->w0; p.w1 = w->w1; p.w2 = w->w2; p.w3 = w->w3;
   p.hits = w->hits;
   p.cand = w->cand;
-  p.so = w->so; p.sd = w->sd; p.sv = w->sv;
+  p.so = w->so; p.sd = w->sd; p.sv = w->sv; p.svis = w->svis;
   p.ctr = w->ctr;
   p.cap_ray = w->cap_ray;
   p.cap_cand = w->cap_cand;
@@ -778,6 +1024,7 @@ int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, i
     if ((rc = launch(c, k_wf_cand, kBlock, 0, p, p.nslots))) return rc;
     if ((rc = launch(c, k_wf_connect, kBlock, 0, p, -1))) return rc;
     if ((rc = stats ? trace_launch<true>(c, p, true, -1) : trace_launch<false>(c, p, true, -1))) return rc;
+    if (wf_refill() && (rc = launch(c, k_wf_resolve, kBlock, 0, p, -1))) return rc;
   }
   return BDPT_OK;
 }
