@@ -30,12 +30,19 @@ HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_NODE, BYTES_TRI, BYTES_SPH, BYTES_HIT = 32, 36, 16, 40
 
 
+def rank_sample_range(step: int, rank: int, world: int, spp: int):
+    """Global sample indices [begin, begin + spp) that `rank` renders in `step`: every step and
+    rank owns a fresh range, so the N-GPU image equals a single render of N*spp samples (sample
+    keys are global)."""
+    return (step * world + rank) * spp, spp
+
+
 def algorithmic_bytes(st) -> int:
     return (BYTES_NODE * st.node_visits + BYTES_TRI * st.tri_tests + BYTES_SPH * st.sph_tests
             + BYTES_HIT * st.hits)
 
 
-def cpu_baseline(scene, threads: int, budget_s: float = 12.0) -> dict:
+def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0) -> dict:
     """The oracle's fp64 reference-semantics path (mode COUNTER64: the reference's arithmetic,
     multi-threaded like the reference's -t N) timed on this host on a bounded sample of the same
     workload (full 480x360 frame, a few spp)."""
@@ -52,7 +59,7 @@ def cpu_baseline(scene, threads: int, budget_s: float = 12.0) -> dict:
         rate = W * H * spp_run / dt
         spp_run = max(1, min(SPP - s0, int((budget_s - t_tot) * rate / (W * H))))
     return {"value": done / t_tot / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{SCENE} {W}x{H}, {done // (W * H)} spp of 128, m={M}, oracle fp64 "
+            "sample": f"{name} {W}x{H}, {done // (W * H)} spp of {SPP}, m={M}, oracle fp64 "
                       f"(reference arithmetic) with {threads} threads, {t_tot:.1f} s"}
 
 
@@ -74,14 +81,23 @@ def parity_check(scene, seed: int) -> dict:
 
 
 def main() -> int:
+    global W, H, SPP, M
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--scene", default=SCENE)
+    ap.add_argument("--scene", default=SCENE,
+                    help="golden scene name (tests/golden/scenes) or a .dae path, e.g. the north-star "
+                         "stand-in scenes/CBlucy_standin.dae")
+    ap.add_argument("--width", type=int, default=W)
+    ap.add_argument("--height", type=int, default=H)
+    ap.add_argument("--spp", type=int, default=SPP)
+    ap.add_argument("--max-depth", type=int, default=M)
+    ap.add_argument("--pipeline", type=int, default=0, help="0 auto, 1 megakernel, 2 wavefront")
     args = ap.parse_args()
+    W, H, SPP, M = args.width, args.height, args.spp, args.max_depth
 
     import numpy as np
     import torch
@@ -100,18 +116,20 @@ def main() -> int:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    scene = golden_scene(args.scene, W, H)
+    scene = (B.load_dae(args.scene, W, H) if args.scene.endswith(".dae")
+             else golden_scene(args.scene, W, H))
     seed = 5489
     stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
     torch.cuda.set_stream(stream)
     # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
-    pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index)
+    pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
+                                   pipeline=args.pipeline)
     pt.set_stream(stream.cuda_stream)
     frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
 
     def step(k: int):
-        base = (k * world + rank) * SPP        # fresh global sample range every step
-        pt.raytrace_tiles([], base, SPP)
+        base, n = rank_sample_range(k, rank, world, SPP)   # fresh global sample range every step
+        pt.raytrace_tiles([], base, n)
         pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
         if dist is not None:
             dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
@@ -126,9 +144,9 @@ def main() -> int:
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
-        base = ((args.warmup + k) * world + rank) * SPP
+        base, n = rank_sample_range(args.warmup + k, rank, world, SPP)
         ev[k][0].record(stream)
-        pt.raytrace_tiles([], base, SPP)            # k_bdpt_sample: the dominant kernel
+        pt.raytrace_tiles([], base, n)              # k_bdpt_sample: the dominant kernel
         ev[k][1].record(stream)
         pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
         if dist is not None:
@@ -148,7 +166,7 @@ def main() -> int:
     # algorithmic bytes of one launch: in-kernel counters on a separate, untimed launch of the
     # same workload (counting perturbs timing), SURVEY.md §8d.
     ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                   collect_stats=True)
+                                   collect_stats=True, pipeline=args.pipeline)
     ps.raytrace_tiles([], rank * SPP, SPP)
     st = ps.stats()
     ps.close()
@@ -158,8 +176,9 @@ def main() -> int:
     samples_total = W * H * SPP * world * args.steps
     value = samples_total / elapsed / 1e6
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")
-    if os.path.exists(tpath):
+    default_workload = (args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5)
+    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")   # PMC pass of this workload
+    if default_workload and os.path.exists(tpath):
         with open(tpath) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
@@ -179,10 +198,12 @@ def main() -> int:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: fixed-seed renders (Philox counter RNG) of the reference's scene "
-                "CBspheres.dae as the reference loads it (tests/golden/scenes)",
-        "config": {"workload": f"{args.scene} {W}x{H} -s {SPP} -m {M} (BASELINE configs[1]) "
+        "data": f"synthetic: fixed-seed renders (Philox counter RNG) of the reference's scene "
+                f"{os.path.basename(args.scene)} as the reference loads it",
+        "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} -s {SPP} -m {M}"
+                               f"{' (BASELINE configs[1])' if default_workload else ''} "
                                f"per GPU, sample-range shards + RCCL sum-reduce",
+                   "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
                    "scene": args.scene, "width": W, "height": H, "spp_per_gpu": SPP,
                    "max_depth": M, "parallelism": f"samples x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
@@ -197,7 +218,7 @@ def main() -> int:
     if world == 1 and not args.no_parity:
         out["parity"] = parity_check(scene, seed)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, threads=min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(scene, args.scene, threads=min(16, os.cpu_count() or 1))
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
