@@ -334,22 +334,25 @@ struct TravStack {
 };
 
 struct RayInv {
-  f3 o, d, inv;
+  f3 o, d, inv, oi;   // oi = o * inv: slab planes are fma(p, inv, -oi)
 };
 BDPT_HD RayInv make_rayinv(f3 o, f3 d) {
   RayInv r;
   r.o = o; r.d = d;
   r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.oi = mk3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
   return r;
 }
 // Slab test against a padded (conservative) box. NaN lanes (0 * inf) are ignored by fmin/fmax.
+// The fused form rounds differently from (p - o) * inv by at most ulp(o * inv) in t, far inside
+// the 2^-16 box padding, so it never culls a box a hit lies in (results do not depend on it).
 BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, float hy, float hz,
                   float* tn, float* tf) {
-  float t0x = (lx - r.o.x) * r.inv.x, t1x = (hx - r.o.x) * r.inv.x;
-  float t0y = (ly - r.o.y) * r.inv.y, t1y = (hy - r.o.y) * r.inv.y;
-  float t0z = (lz_ - r.o.z) * r.inv.z, t1z = (hz - r.o.z) * r.inv.z;
-  float n = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-  float f = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+  const float t0x = fmaf(lx, r.inv.x, -r.oi.x), t1x = fmaf(hx, r.inv.x, -r.oi.x);
+  const float t0y = fmaf(ly, r.inv.y, -r.oi.y), t1y = fmaf(hy, r.inv.y, -r.oi.y);
+  const float t0z = fmaf(lz_, r.inv.z, -r.oi.z), t1z = fmaf(hz, r.inv.z, -r.oi.z);
+  const float n = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+  const float f = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
   *tn = n;
   *tf = f * 1.00000024f;
 }
@@ -460,6 +463,63 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     }
     if (!stk.pop(ref)) return false;
   }
+}
+
+// Resumable forms of the two queries for lane-refill loops: one call = descend to a leaf + test
+// it (same visit order, same results as trace_closest / trace_any); true when the query is done.
+// one leaf visit of a closest-hit query: descend to a leaf, test it; true when finished
+template <int LM, int K>
+BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
+                                             int& ref, TravStack<K>& stk, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
+  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
+  if (ref == kTravDone) return true;
+  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  for (int k = 0; k < cnt; k++) {
+    const int pi = st + k;
+    float t, b1 = 0, b2 = 0;
+    bool ok;
+    int key;
+    if ((sm >> k) & 1) {
+      c.sphs++;
+      ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
+      key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
+    } else {
+      c.tris++;
+      const float4 g2 = GEOM[3 * pi + 2];
+      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
+      key = __float_as_int(g2.y);
+    }
+    if (ok && (t < h.t || key > h.key)) {   // same rule as trace_closest (bdpt_core.h)
+      h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
+    }
+  }
+  return !stk.pop(ref);
+}
+
+// one leaf visit of an any-hit query: true when finished (*hit tells whether something was hit)
+template <int LM, int K>
+BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
+                                         int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
+  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
+  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
+  if (ref == kTravDone) { *hit = false; return true; }
+  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  for (int k = 0; k < cnt; k++) {
+    const int pi = st + k;
+    float t, b1, b2;
+    bool ok;
+    if ((sm >> k) & 1) {
+      c.sphs++;
+      ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
+    } else {
+      c.tris++;
+      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+    }
+    if (ok) { *hit = true; return true; }
+  }
+  if (!stk.pop(ref)) { *hit = false; return true; }
+  return false;
 }
 
 // Shading record of a closest hit: interpolated normal (triangle.cpp:80-82) or sphere normal

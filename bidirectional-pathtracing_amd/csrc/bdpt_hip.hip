@@ -129,6 +129,110 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
   }
 }
 
+// Per-lane cache of one light-image target: splats to the cached pixel are summed in registers
+// and written once at the end of the kernel. A point light's t = 1, s = 1 connections all project
+// to one pixel, so every lane ends up caching it and those splats cost no global atomics at all.
+struct SplatCache {
+  int tgt = -1;
+  float x = 0, y = 0, z = 0;
+  __device__ void add(float* light, int t, float vx, float vy, float vz) {
+    if (tgt < 0) tgt = t;
+    if (t == tgt) {
+      x += vx; y += vy; z += vz;
+      return;
+    }
+    float* p = light + 3 * (size_t)t;
+    atomicAdd(p, vx);
+    atomicAdd(p + 1, vy);
+    atomicAdd(p + 2, vz);
+  }
+  // all 64 lanes: lanes caching the same pixel as the first pending lane are reduced first
+  __device__ void flush(float* light, int lane) {
+    bool on = tgt >= 0;
+#pragma unroll 1
+    for (int round = 0; round < 4; round++) {
+      const unsigned long long m = __ballot(on);
+      if (m == 0) return;
+      const int lead = __builtin_ctzll(m);
+      const int t0 = __shfl(tgt, lead, 64);
+      const bool same = on && tgt == t0;
+      if (__popcll(__ballot(same)) < 2) break;
+      const float sx = wave_sumf(same ? x : 0.0f), sy = wave_sumf(same ? y : 0.0f), sz = wave_sumf(same ? z : 0.0f);
+      if (lane == lead) {
+        float* p = light + 3 * (size_t)t0;
+        atomicAdd(p, sx);
+        atomicAdd(p + 1, sy);
+        atomicAdd(p + 2, sz);
+      }
+      on = on && !same;
+    }
+    if (on) {
+      float* p = light + 3 * (size_t)tgt;
+      atomicAdd(p, x);
+      atomicAdd(p + 1, y);
+      atomicAdd(p + 2, z);
+    }
+  }
+};
+
+// Resolves queued connection rays [head, tail) with lane refill: every lane takes an entry, and a
+// lane whose ray is done takes the next pending one (resumable any_step, bdpt_core.h), so the
+// wave's lanes stay busy until the queue runs dry instead of waiting for the slowest of 64 rays.
+#ifndef BDPT_FLUSH_REFILL
+#define BDPT_FLUSH_REFILL 0   // measured slower on the Cornell-box scenes (more spills)
+#endif
+template <int LM>
+__device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int head, int tail, int lane, float* light,
+                                             Counters& cnt, SplatCache& sc) {
+  int next = head;   // wave-uniform
+  bool active = false;
+  int k = 0, ref = 0;
+  f3 o = splat3(0), d = splat3(0);
+  float tmax = 0;
+  RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
+  int stack_mem[BDPT_STACK];
+  TravStack<0> stk(stack_mem);
+  for (;;) {
+    const unsigned long long idle = __ballot(!active);
+    const int take = min(__popcll(idle), tail - next);
+    if (!active) {
+      const int rank = lanes_below(idle);
+      if (rank < take) {
+        k = (next + rank) & (QCAP - 1);
+        o = mk3(q.ox[k], q.oy[k], q.oz[k]);
+        d = mk3(q.dx[k], q.dy[k], q.dz[k]);
+        tmax = q.tmax[k];
+        r = make_rayinv(o, d);
+        ref = S.root;
+        stk.msp = 0;
+        cnt.shadow++;
+        active = true;
+      }
+    }
+    next += take;
+    if (__ballot(active) == 0) break;
+    for (;;) {
+      bool hit = false;
+      if (active && any_step<LM, 0>(S, r, o, d, BDPT_EPS_F, tmax, ref, stk, &hit, cnt)) {
+        active = false;
+        if (!hit) {
+          const int tgt = q.tgt[k];
+          if (tgt < 0) {
+            const int ow = ~tgt;
+            atomicAdd(&q.acc[0][ow], q.vx[k]);
+            atomicAdd(&q.acc[1][ow], q.vy[k]);
+            atomicAdd(&q.acc[2][ow], q.vz[k]);
+          } else {
+            sc.add(light, tgt, q.vx[k], q.vy[k], q.vz[k]);
+          }
+        }
+      }
+      const int na = __popcll(__ballot(active));
+      if (na == 0 || (na <= 56 && next < tail)) break;
+    }
+  }
+}
+
 // k_bdpt_sample: each lane owns one pixel and a chunk of its samples. Per sample the lane builds
 // both subpaths (random walks, closest-hit traversal) and then enumerates its (i, j) connections
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
@@ -162,6 +266,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     kp.S.lgeom = sc + nn;
   }
   Counters cnt = {0, 0, 0, 0, 0, 0};
+  SplatCache sc;
   unsigned nsamp = 0;
   const float inv = 1.0f / (float)kp.sp.spp;
   Paths<MAXV> P;
@@ -256,9 +361,15 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
           PH_STAMP(tp0);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
+#if BDPT_FLUSH_REFILL
+          flush_refill<LM>(kp.S, q, head, tail, lane, kp.light, cnt, sc);
+          __builtin_amdgcn_wave_barrier();
+          head = tail;
+#else
           flush_queue<LM>(kp.S, q, head, 64, lane, kp.light, cnt);
           __builtin_amdgcn_wave_barrier();
           head += 64;
+#endif
           PH_STAMP(tp1);
   #ifdef BDPT_PHASE_PROF
           ph_flush += tp1 - tp0;
@@ -272,7 +383,11 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     if (tail > head) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+#if BDPT_FLUSH_REFILL
+      flush_refill<LM>(kp.S, q, head, tail, lane, kp.light, cnt, sc);
+#else
       flush_queue<LM>(kp.S, q, head, tail - head, lane, kp.light, cnt);
+#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -285,6 +400,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     }
     __builtin_amdgcn_wave_barrier();
   }
+  sc.flush(kp.light, lane);
 #ifdef BDPT_PHASE_PROF
   if (lane == 0) {
     atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);

@@ -652,61 +652,6 @@ struct WavePool {
   __device__ bool more(const QView& qv) const { return count > 0 || next < qv.total; }
 };
 
-// one leaf visit of a closest-hit query: descend to a leaf, test it; true when finished
-template <int LM, int K>
-__device__ __forceinline__ bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
-                                             int& ref, TravStack<K>& stk, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
-  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
-  if (ref == kTravDone) return true;
-  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-  for (int k = 0; k < cnt; k++) {
-    const int pi = st + k;
-    float t, b1 = 0, b2 = 0;
-    bool ok;
-    int key;
-    if ((sm >> k) & 1) {
-      c.sphs++;
-      ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
-      key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
-    } else {
-      c.tris++;
-      const float4 g2 = GEOM[3 * pi + 2];
-      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
-      key = __float_as_int(g2.y);
-    }
-    if (ok && (t < h.t || key > h.key)) {   // same rule as trace_closest (bdpt_core.h)
-      h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
-    }
-  }
-  return !stk.pop(ref);
-}
-
-// one leaf visit of an any-hit query: true when finished (*hit tells whether something was hit)
-template <int LM, int K>
-__device__ __forceinline__ bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
-                                         int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
-  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
-  if (ref == kTravDone) { *hit = false; return true; }
-  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-  for (int k = 0; k < cnt; k++) {
-    const int pi = st + k;
-    float t, b1, b2;
-    bool ok;
-    if ((sm >> k) & 1) {
-      c.sphs++;
-      ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
-    } else {
-      c.tris++;
-      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
-    }
-    if (ok) { *hit = true; return true; }
-  }
-  if (!stk.pop(ref)) { *hit = false; return true; }
-  return false;
-}
-
 template <int LM, bool STATS>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_rf(WfParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
