@@ -1,10 +1,7 @@
 cd "$(dirname "$0")/.." || exit 1
-timeout -k 10 400 python3 -m pytest tests/test_gpu_parity.py -x -q 2>&1 | tail -2
-for cfg in "CBspheres 480 360 128 5 2" "scenes/CBlucy_standin.dae 1920 1080 8 5 2" "CBgems 480 360 64 5 2"; do
-  for lib in build_var_a.so build_var_b.so; do
-  for pipe in 1 2; do
-  echo "== $cfg $lib $pipe"
-  BDPT_LIB=$PWD/$lib BDPT_WF_SLOTS=4194304 BDPT_PIPELINE=$pipe timeout -k 10 300 python3 tools/prof_render.py $cfg || { echo STOP; exit 1; }
-  done
-  done
-done
+timeout -k 10 600 python3 bench.py --scene scenes/CBlucy_standin.dae --width 1920 --height 1080 --spp 128 --steps 2 --warmup 1 > gpurun_out/bench_lucy1080.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_lucy1080.log
+timeout -k 10 600 python3 bench.py --scene scenes/CBlucy_standin.dae --width 800 --height 600 --spp 128 --steps 3 --warmup 1 > gpurun_out/bench_lucy800.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_lucy800.log
+timeout -k 10 600 python3 bench.py --scene scenes/CBgems.dae --width 1920 --height 1080 --spp 256 --max-depth 7 --steps 1 --warmup 1 --no-parity > gpurun_out/bench_gems1080.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_gems1080.log
