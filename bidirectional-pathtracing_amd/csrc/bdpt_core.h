@@ -364,10 +364,39 @@ BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, floa
 // plain loop, so hits and counters do not change.
 constexpr int kTravDone = (int)0x80000000;   // not a valid leaf reference (start would be 2^24)
 
-template <int K>
+// Scene fetches with explicit address spaces on the device: the LDS copy is read with ds_read and
+// the HBM arrays with global_load (through a generic pointer both would compile to flat_load).
+BDPT_HD float4 ld_lds4(const float4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(3))) float4*)p;
+#else
+  return *p;
+#endif
+}
+BDPT_HD float4 ld_glb4(const float4* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(1))) float4*)p;
+#else
+  return *p;
+#endif
+}
+// geometry record k (3 float4 per primitive): LDS copy in LDS mode 1, else HBM
+template <int LM>
+BDPT_HD float4 ld_geom(const SceneView& S, int k) {
+  return LM == 1 ? ld_lds4(S.lgeom + k) : ld_glb4(S.geom + k);
+}
+
+template <int K, int LM>
 BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
-                      const float4* N, Counters& c) {
-  const float4 a = N[0], b = N[1], cc = N[2], e = N[3];
+                      Counters& c) {
+  float4 a, b, cc, e;
+  if (LM == 1 || (LM == 2 && ref < S.ntop)) {
+    const float4* N = S.lnodes + 4 * ref;
+    a = ld_lds4(N); b = ld_lds4(N + 1); cc = ld_lds4(N + 2); e = ld_lds4(N + 3);
+  } else {
+    const float4* N = S.nodes + 4 * ref;
+    a = ld_glb4(N); b = ld_glb4(N + 1); cc = ld_glb4(N + 2); e = ld_glb4(N + 3);
+  }
   c.nodes += 2;
   float tnl, tfl, tnr, tfr;
   slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
@@ -386,15 +415,10 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
   return stk.pop(nx) ? nx : kTravDone;
 }
 
-template <int LM>
-BDPT_HD const float4* node_ptr(const SceneView& S, int ref) {
-  return LM == 1 ? S.lnodes + 4 * ref : LM == 2 && ref < S.ntop ? S.lnodes + 4 * ref : S.nodes + 4 * ref;
-}
 
 // Closest hit in [tmin, tmax]; ties in t go to the larger DFS position (reference order).
 template <int LM = 0, int K = 0>
 BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Hit& h, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
   h.t = tmax;
   h.prim = -1;
@@ -405,7 +429,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   int ref = S.root;
   c.closest++;
   for (;;) {
-    while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
+    while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
     if (ref == kTravDone) break;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
     for (int k = 0; k < cnt; k++) {
@@ -415,12 +439,12 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       int key;
       if ((sm >> k) & 1) {
         c.sphs++;
-        ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
-        key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
+        ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
+        key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
       } else {
         c.tris++;
-        const float4 g2 = GEOM[3 * pi + 2];
-        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
+        const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
+        ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
         key = __float_as_int(g2.y);
       }
       // t <= h.t here; an equal t replaces the hit only if it comes later in the reference's DFS
@@ -438,14 +462,13 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
 // Any hit in [tmin, tmax] (connection rays, bidirection.cpp:418-433).
 template <int LM = 0, int K = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
   RayInv r = make_rayinv(o, d);
   int stack_mem[BDPT_STACK];
   TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.shadow++;
   for (;;) {
-    while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
+    while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, tmax, stk, c);
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
     for (int k = 0; k < cnt; k++) {
@@ -454,10 +477,10 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       bool ok;
       if ((sm >> k) & 1) {
         c.sphs++;
-        ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
+        ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, tmax, &t);
       } else {
         c.tris++;
-        ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+        ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), ld_geom<LM>(S, 3 * pi + 2), o, d, tmin, tmax, &t, &b1, &b2);
       }
       if (ok) return true;
     }
@@ -471,8 +494,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
 template <int LM, int K>
 BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
                                              int& ref, TravStack<K>& stk, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
-  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, h.t, stk, node_ptr<LM>(S, ref), c);
+  while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
   if (ref == kTravDone) return true;
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -482,12 +504,12 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
     int key;
     if ((sm >> k) & 1) {
       c.sphs++;
-      ok = sph_test(GEOM[3 * pi], o, d, tmin, h.t, &t);
-      key = ok ? __float_as_int(GEOM[3 * pi + 1].x) : 0;
+      ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
+      key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
     } else {
       c.tris++;
-      const float4 g2 = GEOM[3 * pi + 2];
-      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], g2, o, d, tmin, h.t, &t, &b1, &b2);
+      const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
+      ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
       key = __float_as_int(g2.y);
     }
     if (ok && (t < h.t || key > h.key)) {   // same rule as trace_closest (bdpt_core.h)
@@ -501,8 +523,7 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
 template <int LM, int K>
 BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
                                          int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  const float4* GEOM = LM == 1 ? S.lgeom : S.geom;
-  while (ref >= 0) ref = node_step<K>(S, r, ref, tmin, tmax, stk, node_ptr<LM>(S, ref), c);
+  while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, tmax, stk, c);
   if (ref == kTravDone) { *hit = false; return true; }
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -511,10 +532,10 @@ BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmi
     bool ok;
     if ((sm >> k) & 1) {
       c.sphs++;
-      ok = sph_test(GEOM[3 * pi], o, d, tmin, tmax, &t);
+      ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, tmax, &t);
     } else {
       c.tris++;
-      ok = tri_test(GEOM[3 * pi], GEOM[3 * pi + 1], GEOM[3 * pi + 2], o, d, tmin, tmax, &t, &b1, &b2);
+      ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), ld_geom<LM>(S, 3 * pi + 2), o, d, tmin, tmax, &t, &b1, &b2);
     }
     if (ok) { *hit = true; return true; }
   }
@@ -526,10 +547,10 @@ BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmi
 // (sphere.cpp:78-81), and the material.
 BDPT_HD void shade_hit(const SceneView& S, const Hit& h, f3 o, f3 d, f3* n_out, int* mat_out) {
   const float4* sh = S.shade + 3 * h.prim;
-  float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
+  float4 s0 = ld_glb4(sh), s1 = ld_glb4(sh + 1), s2 = ld_glb4(sh + 2);
   *mat_out = __float_as_int(s2.y);
   if (__float_as_int(s2.z) != 0) {   // sphere: center in geom
-    float4 g = S.geom[3 * h.prim];
+    float4 g = ld_glb4(S.geom + 3 * h.prim);
     f3 p = add(o, smul(h.t, d));
     *n_out = normalize(sub(p, mk3(g.x, g.y, g.z)));
   } else {
