@@ -198,7 +198,7 @@ BDPT_HD int leaf_count(int r) { return (int)((uint32_t)~r & 7u); }
 BDPT_HD int leaf_sph_mask(int r) { return (int)((((uint32_t)~r) >> 3) & 15u); }
 
 struct SceneView {
-  const float4* nodes;   // 4 x float4 per node: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
+  const float4* nodes;   // node_f4(lm_width(LM)) float4 per node (layouts at node_step)
   const float4* geom;    // 3 x float4 per prim (DFS order): tri p0,e1,e2 | sphere c,r
   const float4* shade;   // 3 x float4 per prim: n1 n2 n3 (tri) ; w of the 3rd = material (bits)
   const DMat* mats;
@@ -298,6 +298,23 @@ namespace bdpt {
 #ifndef BDPT_STACK
 #define BDPT_STACK 64
 #endif
+// Children per BVH node: 2 (64-B nodes) or 4 (128-B nodes: half the dependent node fetches per
+// ray, four independent slab tests per fetch). The host emits both trees over the same leaves;
+// a kernel traverses the one its LDS mode selects: scenes fetched from HBM (LM 0, LM 2's nodes below
+// the treelet) gain from the shorter dependent chain, a scene held whole in LDS (LM 1) does not
+// (its fetches are short, and the wider test costs instructions). Measured, DESIGN.md §5.
+#ifndef BDPT_BVH_WIDTH
+#define BDPT_BVH_WIDTH 4       // LM 0 / 2
+#endif
+#ifndef BDPT_LDS_BVH_WIDTH
+#define BDPT_LDS_BVH_WIDTH 2   // LM 1
+#endif
+static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
+              "BVH widths must be 2 or 4");
+BDPT_HD constexpr int lm_width(int LM) { return LM == 1 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
+BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
+BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
+BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
 // ones in a private array. K = 0 keeps the whole stack in the array (megakernel: its VGPR budget is
@@ -385,36 +402,120 @@ template <int LM>
 BDPT_HD float4 ld_geom(const SceneView& S, int k) {
   return LM == 1 ? ld_lds4(S.lgeom + k) : ld_glb4(S.geom + k);
 }
+// A node from the LDS copy: one asm block of ds_read_b128 and a single wait. Written out because a
+// node fetch that may come from LDS or HBM (treelet mode) otherwise compiles to flat_load for both.
+template <int W>
+BDPT_HD void ld_node_lds(const float4* p, float4* v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)p;
+  v4f t[7];
+  if (W == 4) {
+    asm volatile(
+        "ds_read_b128 %0, %7\n\t"
+        "ds_read_b128 %1, %7 offset:16\n\t"
+        "ds_read_b128 %2, %7 offset:32\n\t"
+        "ds_read_b128 %3, %7 offset:48\n\t"
+        "ds_read_b128 %4, %7 offset:64\n\t"
+        "ds_read_b128 %5, %7 offset:80\n\t"
+        "ds_read_b128 %6, %7 offset:96\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
+        : "v"(a));
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:16\n\t"
+        "ds_read_b128 %2, %4 offset:32\n\t"
+        "ds_read_b128 %3, %4 offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+        : "v"(a));
+  }
+#pragma unroll
+  for (int k = 0; k < node_used_f4(W); k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
+#else
+  for (int k = 0; k < node_used_f4(W); k++) v[k] = p[k];
+#endif
+}
 
+// One node of the descent: slab-test the children, continue with the nearest hit child, push the
+// other hit children (farther first, so they pop near-first); pop when none is hit.
+// Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
+// Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad
 template <int K, int LM>
 BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
                       Counters& c) {
-  float4 a, b, cc, e;
-  if (LM == 1 || (LM == 2 && ref < S.ntop)) {
-    const float4* N = S.lnodes + 4 * ref;
-    a = ld_lds4(N); b = ld_lds4(N + 1); cc = ld_lds4(N + 2); e = ld_lds4(N + 3);
+  constexpr int W = lm_width(LM), NU = node_used_f4(W);
+  float4 v[NU];
+  if (LM == 1) {   // all nodes in LDS: plain ds_reads the compiler schedules
+#pragma unroll
+    for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
+  } else if (LM == 2 && ref < S.ntop) {
+    ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
   } else {
-    const float4* N = S.nodes + 4 * ref;
-    a = ld_glb4(N); b = ld_glb4(N + 1); cc = ld_glb4(N + 2); e = ld_glb4(N + 3);
+#pragma unroll
+    for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
   }
-  c.nodes += 2;
-  float tnl, tfl, tnr, tfr;
-  slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
-  slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
-  const bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
-  const bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
-  const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
-  if (hl && hr) {
-    const bool lfirst = tnl <= tnr;
-    stk.push(lfirst ? rref : lref);
-    return lfirst ? lref : rref;
+  if (W == 2) {
+    const float4 a = v[0], b = v[1], cc = v[2], e = v[3 % NU];
+    c.nodes += 2;
+    float tnl, tfl, tnr, tfr;
+    slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
+    slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
+    const bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
+    const bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
+    const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
+    if (hl && hr) {
+      const bool lfirst = tnl <= tnr;
+      stk.push(lfirst ? rref : lref);
+      return lfirst ? lref : rref;
+    }
+    if (hl) return lref;
+    if (hr) return rref;
+    int nx;
+    return stk.pop(nx) ? nx : kTravDone;
+  } else {
+    const float4 lx = v[0], hx = v[1], ly = v[2 % NU], hy = v[3 % NU];
+    const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
+    c.nodes += 4;
+    // sort key: entry distance of a hit child, +inf for a miss or an empty slot
+    float k0, k1, k2, k3;
+    int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y), r2 = __float_as_int(e.z), r3 = __float_as_int(e.w);
+    {
+      float tn, tf;
+      slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn, &tf);
+      k0 = (r0 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
+      slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn, &tf);
+      k1 = (r1 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
+      slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn, &tf);
+      k2 = (r2 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
+      slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn, &tf);
+      k3 = (r3 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
+    }
+    // 5-comparator sorting network on (key, ref)
+#define BDPT_CSWAP(ka, ra, kb, rb)                          \
+  {                                                         \
+    const bool sw = kb < ka;                                \
+    const float tk = sw ? kb : ka; kb = sw ? ka : kb; ka = tk; \
+    const int tr = sw ? rb : ra; rb = sw ? ra : rb; ra = tr;   \
   }
-  if (hl) return lref;
-  if (hr) return rref;
-  int nx;
-  return stk.pop(nx) ? nx : kTravDone;
+    BDPT_CSWAP(k0, r0, k1, r1);
+    BDPT_CSWAP(k2, r2, k3, r3);
+    BDPT_CSWAP(k0, r0, k2, r2);
+    BDPT_CSWAP(k1, r1, k3, r3);
+    BDPT_CSWAP(k1, r1, k2, r2);
+#undef BDPT_CSWAP
+    if (!(k0 < INFINITY)) {
+      int nx;
+      return stk.pop(nx) ? nx : kTravDone;
+    }
+    if (k3 < INFINITY) stk.push(r3);
+    if (k2 < INFINITY) stk.push(r2);
+    if (k1 < INFINITY) stk.push(r1);
+    return r0;
+  }
 }
-
 
 // Closest hit in [tmin, tmax]; ties in t go to the larger DFS position (reference order).
 template <int LM = 0, int K = 0>
@@ -1199,11 +1300,11 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
 
 // One pixel-sample, connections resolved in the reference's (i, j) order (host/test use; the
 // device kernel defers the connection rays to a wave-compacted queue instead).
-template <int MAXV, class Sink>
+template <int MAXV, int LM = 0, class Sink>
 BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt,
                          int x, int y, uint32_t sample, Sink& sink) {
   Rng g;
-  prepare_sample<MAXV>(S, sp, P, cnt, g, x, y, sample);
+  prepare_sample<MAXV, LM>(S, sp, P, cnt, g, x, y, sample);
   f3 eye_sum = splat3(0);
   for (int i = 1; i < P.nE; i++) {
     for (int j = 0; j < P.nL; j++) {
@@ -1212,7 +1313,7 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
       if (kind == CONN_DIRECT) {
         eye_sum = add(eye_sum, cn.val);
       } else if (kind == CONN_RAY) {
-        if (trace_any(S, cn.o, cn.d, BDPT_EPS_F, cn.tmax, cnt)) continue;
+        if (trace_any<LM>(S, cn.o, cn.d, BDPT_EPS_F, cn.tmax, cnt)) continue;
         if (cn.splat >= 0) sink.splat(cn.splat % sp.W, cn.splat / sp.W, cn.val);
         else eye_sum = add(eye_sum, cn.val);
       }

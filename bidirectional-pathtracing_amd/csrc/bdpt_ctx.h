@@ -27,7 +27,8 @@ struct Ctx {
   hipStream_t own = nullptr, stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
-  float* d_nodes = nullptr;
+  float* d_nodes2 = nullptr;   // HostScene::bvh2 / bvh4
+  float* d_nodes4 = nullptr;
   float* d_geom = nullptr;
   float* d_shade = nullptr;
   DMat* d_mats = nullptr;
@@ -56,15 +57,17 @@ struct Ctx {
     }                                                                               \
   } while (0)
 
-inline SceneView view_of(const Ctx* c) {
+// The scene as a kernel of LDS mode LM sees it (its tree width: lm_width(LM)).
+inline SceneView view_of(const Ctx* c, int LM) {
   SceneView S;
-  S.nodes = (const float4*)c->d_nodes;
+  const int W = lm_width(LM);
+  S.nodes = (const float4*)(W == 4 ? c->d_nodes4 : c->d_nodes2);
   S.geom = (const float4*)c->d_geom;
   S.shade = (const float4*)c->d_shade;
   S.mats = c->d_mats;
   S.lights = c->d_lights;
   S.nlights = (int)c->hs.lights.size();
-  S.root = c->hs.root;
+  S.root = c->hs.tree(W).root;
   S.lnodes = nullptr;
   S.lgeom = nullptr;
   S.ntop = 0;

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   WaveQ& q = qs[threadIdx.x >> 6];
   if (LM != 0) {
     float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
-    const int nn = LM == 1 ? kp.n_node4 : 4 * kp.S.ntop;
+    const int nn = LM == 1 ? kp.n_node4 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
       sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
@@ -465,16 +465,17 @@ int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
 template <int MAXV, bool STATS>
 int launch_lm(Ctx* c, KParams& kp) {
   const size_t q = kWavesPerBlock * sizeof(WaveQ);
-  const size_t full = (size_t)(kp.n_node4 + kp.n_geom4) * 16;
+  const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
+  const bool has_nodes = !c->hs.bvh2.nodes.empty();
   const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2
-  int lm = env ? atoi(env) : (full <= kLdsSceneMax ? 1 : kp.n_node4 > 0 ? 2 : 0);
+  int lm = env ? atoi(env) : (full <= kLdsSceneMax ? 1 : has_nodes ? 2 : 0);
   if (lm == 1 && full > kLdsSceneMax) lm = 2;
-  if (lm == 2) {
-    kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.n_top, kLdsSceneMax / 64);
-    if (kp.S.ntop <= 0) lm = 0;
-  }
+  if (lm == 2 && !has_nodes) lm = 0;
+  kp.S = view_of(c, lm);
+  kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
+  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
   if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1>, q + full, kp);
-  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2>, q + (size_t)kp.S.ntop * 64, kp);
+  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
   return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0>, q, kp);
 }
 
@@ -485,7 +486,7 @@ int launch_maxv(Ctx* c, KParams& kp) {
 
 void free_ctx(Ctx* c) {
   if (!c) return;
-  void* bufs[] = {c->d_nodes, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref,
+  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref,
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -544,7 +545,8 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if (hipSetDevice(c->device) != hipSuccess) { g_err = "hipSetDevice failed"; return fail(BDPT_E_DEVICE); }
   if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->ncu <= 0)
     c->ncu = 256;
-  if ((rc = upload(&c->d_nodes, c->hs.nodes))) return fail(rc);
+  if ((rc = upload(&c->d_nodes2, c->hs.bvh2.nodes))) return fail(rc);
+  if ((rc = upload(&c->d_nodes4, c->hs.bvh4.nodes))) return fail(rc);
   if ((rc = upload(&c->d_geom, c->hs.geom))) return fail(rc);
   if ((rc = upload(&c->d_shade, c->hs.shade))) return fail(rc);
   if ((rc = upload(&c->d_mats, c->hs.mats))) return fail(rc);
@@ -606,13 +608,12 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   HIPCHK(hipSetDevice(c->device));
   const int W = c->prm.width, H = c->prm.height;
   KParams kp;
-  kp.S = view_of(c);
+  kp.S = view_of(c, 0);   // launch_lm sets the LDS mode's view
   kp.sp.W = W; kp.sp.H = H; kp.sp.spp = c->prm.spp; kp.sp.max_depth = c->prm.max_depth; kp.sp.seed = c->prm.seed;
   kp.eye = c->d_eye;
   kp.light = c->d_light;
   kp.stats = c->d_stats;
   kp.prof = c->d_stats + 8;
-  kp.n_node4 = (int)(c->hs.nodes.size() / 4);
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
@@ -762,7 +763,7 @@ int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, fl
   HIPCHK(hipMalloc((void**)&d_t, (size_t)n * sizeof(float)));
   HIPCHK(hipMalloc((void**)&d_p, (size_t)n * sizeof(int)));
   HIPCHK(hipMemcpy(d_r, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_trace_rays, dim3((n + 127) / 128), dim3(128), 0, c->stream, view_of(c), d_r, n, any_hit,
+  hipLaunchKernelGGL(k_trace_rays, dim3((n + 127) / 128), dim3(128), 0, c->stream, view_of(c, 0), d_r, n, any_hit,
                      d_t, d_p, c->d_prim_ref);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));

@@ -324,7 +324,6 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
   Builder& T = use_ref ? R : Bs;
   out.dev_depth = T.depth;
   out.dev_nodes = (int)T.nodes.size();
-  if (T.depth + 2 > BDPT_STACK) { err = "BVH deeper than the traversal stack"; return BDPT_E_UNSUPPORTED; }
 
   // primitives in the device tree's DFS leaf order
   out.prim_ref = T.leaf_prims;
@@ -354,62 +353,115 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
       S[10] = i2f(1);
     }
   }
-  // nodes: the top kTopNodes internal nodes in BFS order (the LDS treelet: every ray starts
-  // there), then the rest in DFS pre-order (subtrees contiguous for the global fetches).
-  std::vector<int> dev_index(T.nodes.size(), -1);
-  std::vector<int> order;
-  if (T.nodes[root].l >= 0) {
-    std::vector<int> bfs{root};
-    for (size_t h = 0; h < bfs.size() && (int)order.size() < kTopNodes; h++) {
-      int id = bfs[h];
-      dev_index[id] = (int)order.size();
-      order.push_back(id);
-      for (int ch : {T.nodes[id].l, T.nodes[id].r})
-        if (T.nodes[ch].l >= 0) bfs.push_back(ch);
-    }
-    out.n_top = (int)order.size();
-    std::vector<int> st{root};
-    while (!st.empty()) {
-      int id = st.back();
-      st.pop_back();
-      if (dev_index[id] < 0) {
+  for (int W : {2, 4}) {
+    HostBvh& B = W == 4 ? out.bvh4 : out.bvh2;
+    // Wide nodes (W children): each binary internal node that starts a wide node pulls in
+    // the grandchildren of its largest-area internal children until it has W of them.
+    auto sarea = [](const Box& b) {
+      const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+      return 2 * (dx * dy + dy * dz + dz * dx);
+    };
+    auto children = [&](int id) {
+      std::vector<int> ch{T.nodes[id].l, T.nodes[id].r};
+      while ((int)ch.size() < W) {
+        int best = -1;
+        double ba = -1;
+        for (size_t k = 0; k < ch.size(); k++)
+          if (T.nodes[ch[k]].l >= 0 && sarea(T.nodes[ch[k]].box) > ba) { ba = sarea(T.nodes[ch[k]].box); best = (int)k; }
+        if (best < 0) break;
+        const int x = ch[best];
+        ch[best] = T.nodes[x].l;
+        ch.insert(ch.begin() + best + 1, T.nodes[x].r);
+      }
+      return ch;
+    };
+    // node order: the top kTopNodes wide nodes in BFS order (the LDS treelet: every ray starts
+    // there), then the rest in DFS pre-order (subtrees contiguous for the global fetches).
+    std::vector<int> dev_index(T.nodes.size(), -1);
+    std::vector<int> order;
+    std::vector<std::vector<int>> kids;   // per emitted node, its binary child ids
+    int wdepth = 0;
+    if (T.nodes[root].l >= 0) {
+      std::vector<int> bfs{root};
+      for (size_t h = 0; h < bfs.size() && (int)order.size() < kTopNodes; h++) {
+        int id = bfs[h];
         dev_index[id] = (int)order.size();
         order.push_back(id);
+        kids.push_back(children(id));
+        for (int ch : kids.back())
+          if (T.nodes[ch].l >= 0) bfs.push_back(ch);
       }
-      if (T.nodes[T.nodes[id].r].l >= 0) st.push_back(T.nodes[id].r);
-      if (T.nodes[T.nodes[id].l].l >= 0) st.push_back(T.nodes[id].l);
+      B.n_top = (int)order.size();
+      std::vector<std::pair<int, int>> st{{root, 0}};
+      while (!st.empty()) {
+        const int id = st.back().first, dd = st.back().second;
+        st.pop_back();
+        wdepth = std::max(wdepth, dd);
+        if (dev_index[id] < 0) {
+          dev_index[id] = (int)order.size();
+          order.push_back(id);
+          kids.push_back(children(id));
+        }
+        const std::vector<int>& ch = kids[dev_index[id]];
+        for (int k = (int)ch.size() - 1; k >= 0; k--)
+          if (T.nodes[ch[k]].l >= 0) st.push_back({ch[k], dd + 1});
+      }
     }
-  }
-  auto ref_of = [&](int id) -> int {
-    const Node& nd = T.nodes[id];
-    if (nd.l >= 0) return dev_index[id];
-    int mask = 0;
-    for (int k = 0; k < nd.count; k++) {
-      int i = T.leaf_prims[nd.start + k];
-      if (d->prim_type[i] == BDPT_PRIM_SPHERE) mask |= 1 << k;
+    B.depth = wdepth;
+    if ((W - 1) * (wdepth + 1) + 2 > BDPT_STACK) {
+      err = "BVH deeper than the traversal stack";
+      return BDPT_E_UNSUPPORTED;
     }
-    uint32_t enc = ((uint32_t)nd.start << 7) | ((uint32_t)mask << 3) | (uint32_t)nd.count;
-    return (int)~enc;
-  };
-  out.nodes.assign(16 * order.size(), 0.0f);
-  for (size_t k = 0; k < order.size(); k++) {
-    const Node& nd = T.nodes[order[k]];
-    float* N = &out.nodes[16 * k];
-    const Box* cb[2] = {&T.nodes[nd.l].box, &T.nodes[nd.r].box};
-    float v[12];
-    for (int s = 0; s < 2; s++) {
-      const Box& b = *cb[s];
+    auto ref_of = [&](int id) -> int {
+      const Node& nd = T.nodes[id];
+      if (nd.l >= 0) return dev_index[id];
+      int mask = 0;
+      for (int k = 0; k < nd.count; k++) {
+        int i = T.leaf_prims[nd.start + k];
+        if (d->prim_type[i] == BDPT_PRIM_SPHERE) mask |= 1 << k;
+      }
+      uint32_t enc = ((uint32_t)nd.start << 7) | ((uint32_t)mask << 3) | (uint32_t)nd.count;
+      return (int)~enc;
+    };
+    // padded fp32 child boxes: lo.xyz, hi.xyz
+    auto child_box = [&](int id, float v[6]) {
+      const Box& b = T.nodes[id].box;
       double ext = std::max(b.mx[0] - b.mn[0], std::max(b.mx[1] - b.mn[1], b.mx[2] - b.mn[2]));
       for (int c3 = 0; c3 < 3; c3++) {
-        v[6 * s + c3] = pad_down(b.mn[c3], ext);
-        v[6 * s + 3 + c3] = pad_up(b.mx[c3], ext);
+        v[c3] = pad_down(b.mn[c3], ext);
+        v[3 + c3] = pad_up(b.mx[c3], ext);
+      }
+    };
+    B.nodes.assign((size_t)4 * node_f4(W) * order.size(), 0.0f);
+    for (size_t k = 0; k < order.size(); k++) {
+      float* N = &B.nodes[(size_t)4 * node_f4(W) * k];
+      const std::vector<int>& ch = kids[k];
+      if (W == 2) {
+        // lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
+        child_box(ch[0], N);
+        child_box(ch[1], N + 6);
+        N[12] = i2f(ref_of(ch[0]));
+        N[13] = i2f(ref_of(ch[1]));
+      } else {
+        // SoA over the children: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] | refs[4] | pad;
+        // an empty slot has ref kTravDone and a zero box (never read)
+        for (int s = 0; s < W; s++) {
+          float v[6] = {0, 0, 0, 0, 0, 0};
+          int rf = kTravDone;
+          if (s < (int)ch.size()) {
+            child_box(ch[s], v);
+            rf = ref_of(ch[s]);
+          }
+          for (int c3 = 0; c3 < 3; c3++) {
+            N[8 * c3 + s] = v[c3];
+            N[8 * c3 + 4 + s] = v[3 + c3];
+          }
+          N[24 + s] = i2f(rf);
+        }
       }
     }
-    for (int c3 = 0; c3 < 12; c3++) N[c3] = v[c3];
-    N[12] = i2f(ref_of(nd.l));
-    N[13] = i2f(ref_of(nd.r));
+    B.root = ref_of(root);
   }
-  out.root = ref_of(root);
   return BDPT_OK;
 }
 

@@ -4,8 +4,10 @@
 // construct_bvh (bvh.cpp:51-129): the BVH topology is the reference's (longest centroid axis,
 // spatial midpoint, leaf <= 4, stable partition, built in fp64 on the reference's bboxes), then
 // flattened for HBM:
-//   nodes : 64 B per internal node = both children's fp32 AABBs (outward-rounded and padded by
-//           2^-16 of the box scale, so the fp32 slab test is conservative) + two child refs
+//   nodes : per tree width W (2 and 4, the second collapsed from the first; same leaves), one
+//           node_bytes(W) record per node = the children's fp32 AABBs (outward-rounded and padded
+//           by 2^-16 of the box scale, so the fp32 slab test is conservative) + child refs; the
+//           layouts are at node_step (bdpt_core.h)
 //   geom  : 48 B per primitive in DFS leaf order (triangle p0,e1,e2 | sphere c,r)
 //   shade : 48 B per primitive (triangle n1,n2,n3 | sphere flag) + material id
 //   prim_ref: DFS position -> reference primitive index
@@ -21,8 +23,16 @@
 
 namespace bdpt {
 
+struct HostBvh {
+  std::vector<float> nodes;   // 4 * node_f4(W) floats per node
+  int root = 0;               // root child reference (node index or encoded leaf)
+  int n_top = 0;              // leading nodes in BFS order (LDS treelet candidates)
+  int depth = 0;              // node levels below the root
+};
+
 struct HostScene {
-  std::vector<float> nodes;   // 16 floats per node
+  HostBvh bvh2, bvh4;         // the device tree with 2 / 4 children per node
+  const HostBvh& tree(int W) const { return W == 4 ? bvh4 : bvh2; }
   std::vector<float> geom;    // 12 floats per prim
   std::vector<float> shade;   // 12 floats per prim
   std::vector<int32_t> prim_ref;    // device DFS position -> scene primitive index
@@ -30,12 +40,10 @@ struct HostScene {
   std::vector<DMat> mats;
   std::vector<DLight> lights;
   DCam cam;
-  int root = 0;               // root child reference (node index or encoded leaf)
   int depth = 0;              // reference BVH depth (root = 0)
   int ref_nodes = 0;          // node count of the reference binary tree
-  int dev_nodes = 0, dev_depth = 0;   // the device tree (SAH by default)
+  int dev_nodes = 0, dev_depth = 0;   // the device tree (SAH by default), binary
   int nprim = 0;
-  int n_top = 0;              // leading nodes in BFS order (LDS treelet candidates)
 };
 
 constexpr int kTopNodes = 1024;

@@ -214,7 +214,7 @@ struct PathsStore {
 template <int LM>
 __device__ __forceinline__ void stage_scene(WfParams& p, float4* sc) {
   if (LM == 0) return;
-  const int nn = LM == 1 ? p.n_node4 : 4 * p.S.ntop;
+  const int nn = LM == 1 ? p.n_node4 : node_f4(lm_width(LM)) * p.S.ntop;
   const int n4 = nn + (LM == 1 ? p.n_geom4 : 0);
   for (int k = threadIdx.x; k < n4; k += blockDim.x) sc[k] = k < nn ? p.S.nodes[k] : p.S.geom[k - nn];
   __syncthreads();
@@ -845,15 +845,15 @@ int wf_alloc(Ctx* c) {
     return rc;
   }
   // LDS staging for the traversal kernels: whole scene if it fits, else the BFS treelet.
-  const size_t full = (c->hs.nodes.size() + c->hs.geom.size()) * sizeof(float);
+  const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const char* lenv = getenv("BDPT_LDS_MODE");
   w->lm = lenv ? atoi(lenv) : (full <= kTraceLds ? 1 : 2);
   if (w->lm == 1 && full > kTraceLds) w->lm = 2;
   if (w->lm == 2) {
-    w->ntop = (int)std::min<size_t>((size_t)c->hs.n_top, kTraceLds / 64);
+    w->ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kTraceLds / node_bytes(lm_width(2)));
     if (w->ntop <= 0) w->lm = 0;
   }
-  w->lds = w->lm == 1 ? full : w->lm == 2 ? (size_t)w->ntop * 64 : 0;
+  w->lds = w->lm == 1 ? full : w->lm == 2 ? (size_t)w->ntop * node_bytes(lm_width(2)) : 0;
   return BDPT_OK;
 }
 
@@ -914,7 +914,7 @@ int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, i
   const bool stats = c->prm.collect_stats != 0;
   WfParams p;
   memset(&p, 0, sizeof p);
-  p.S = view_of(c);
+  p.S = view_of(c, w->lm);
   p.sp.W = c->prm.width; p.sp.H = c->prm.height; p.sp.spp = c->prm.spp; p.sp.max_depth = c->prm.max_depth;
   p.sp.seed = c->prm.seed;
   p.eye = c->d_eye;
@@ -936,7 +936,7 @@ int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, i
   p.cap_ray = w->cap_ray;
   p.cap_cand = w->cap_cand;
   p.cap_sh = w->cap_sh;
-  p.n_node4 = (int)(c->hs.nodes.size() / 4);
+  p.n_node4 = (int)(c->hs.tree(lm_width(w->lm)).nodes.size() / 4);
   p.n_geom4 = (int)(c->hs.geom.size() / 4);
   p.inv_spp = 1.0f / (float)c->prm.spp;
   for (const DLight& l : c->hs.lights) p.point_light |= l.type == LIGHT_POINT;

@@ -18,19 +18,21 @@ struct HostSink {
   }
 };
 
-template <int MAXV>
+template <int MAXV, int LM>
 static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed, int s0, int count,
                const int* pixels, int npix, double* eye, double* light, double* stats) {
   SceneView S;
-  S.nodes = (const float4*)hs.nodes.data();
+  const HostBvh& T = hs.tree(lm_width(LM));
+  S.nodes = (const float4*)T.nodes.data();
   S.geom = (const float4*)hs.geom.data();
   S.shade = (const float4*)hs.shade.data();
   S.mats = hs.mats.data();
   S.lights = hs.lights.data();
   S.nlights = (int)hs.lights.size();
-  S.root = hs.root;
-  S.lnodes = nullptr;
-  S.lgeom = nullptr;
+  S.root = T.root;
+  // LM 1 reads the "LDS copy": on the CPU the same arrays (exercises the LDS-mode tree)
+  S.lnodes = LM == 1 ? S.nodes : nullptr;
+  S.lgeom = LM == 1 ? S.geom : nullptr;
   S.ntop = 0;
   S.cam = hs.cam;
   SampleParams sp;
@@ -44,7 +46,7 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   for (int q = 0; q < total; q++) {
     int x = pixels ? pixels[2 * q] : q % W, y = pixels ? pixels[2 * q + 1] : q / W;
     for (int s = s0; s < s0 + count; s++) {
-      f3 v = render_sample<MAXV>(S, sp, *P, cnt, x, y, (uint32_t)s, sink);
+      f3 v = render_sample<MAXV, LM>(S, sp, *P, cnt, x, y, (uint32_t)s, sink);
       size_t k = 3 * ((size_t)x + (size_t)y * W);
       eye[k] += (double)(v.x * inv); eye[k + 1] += (double)(v.y * inv); eye[k + 2] += (double)(v.z * inv);
     }
@@ -58,17 +60,26 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   return 0;
 }
 
-extern "C" int core_cpu_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
-                               int count, const int* pixels, int npix, double* eye, double* light, double* stats) {
+template <int LM>
+static int render_lm(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
+                     int count, const int* pixels, int npix, double* eye, double* light, double* stats) {
   HostScene hs;
   std::string err;
   int rc = build_host_scene(d, hs, err);
   if (rc) { fprintf(stderr, "core_cpu: %s\n", err.c_str()); return rc; }
   int need = M < 1 ? 1 : M;
-  if (need <= 5) return run<5>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  if (need <= 8) return run<8>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  if (need <= 16) return run<16>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
+  if (need <= 5) return run<5, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
+  if (need <= 8) return run<8, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
+  if (need <= 16) return run<16, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
   return BDPT_E_UNSUPPORTED;
+}
+
+// lds_mode 0: the HBM tree (lm_width(0) children per node); 1: the LDS-mode tree (lm_width(1))
+extern "C" int core_cpu_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
+                               int count, const int* pixels, int npix, double* eye, double* light, double* stats,
+                               int lds_mode) {
+  if (lds_mode == 1) return render_lm<1>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
+  return render_lm<0>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
 }
 
 extern "C" int core_cpu_scene_info(const bdpt_scene_desc* d, int* depth, int* ref_nodes, int* prim_ref) {

@@ -25,14 +25,14 @@ def core():
         P = C.POINTER(C.c_double)
         lib.core_cpu_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int,
-                                        P, P, P]
+                                        P, P, P, C.c_int]
         lib.core_cpu_scene_info.argtypes = [C.POINTER(B.SceneDesc), C.POINTER(C.c_int),
                                             C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _core = lib
     return _core
 
 
-def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None):
+def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None, lds_mode=0):
     lib = core()
     count = spp - s0 if count is None else count
     eye = np.zeros((H, W, 3))
@@ -41,7 +41,7 @@ def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None):
     d = scene.desc()
     pd = C.POINTER(C.c_double)
     rc = lib.core_cpu_render(C.byref(d), W, H, spp, M, seed, s0, count, None, 0,
-                             eye.ctypes.data_as(pd), light.ctypes.data_as(pd), st.ctypes.data_as(pd))
+                             eye.ctypes.data_as(pd), light.ctypes.data_as(pd), st.ctypes.data_as(pd), lds_mode)
     assert rc == 0
     return eye, light, st
 
@@ -51,10 +51,12 @@ CASES = [("CBspheres", 32, 24, 2, 5), ("CBspheres_lambertian", 32, 24, 2, 5), ("
          ("CBspheres", 24, 18, 3, 1)]
 
 
+@pytest.mark.parametrize("lds_mode", [0, 1])
 @pytest.mark.parametrize("name,W,H,spp,M", CASES)
-def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M):
+def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M, lds_mode):
+    """lds_mode 0 traverses the 4-wide tree (HBM kernels), 1 the binary one (scene in LDS)."""
     sc = golden_scene(name, W, H)
-    eye, light, st = core_render(sc, W, H, spp, M, seed=1234)
+    eye, light, st = core_render(sc, W, H, spp, M, seed=1234, lds_mode=lds_mode)
     _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=1234, threads=1)
     assert np.isfinite(eye).all() and np.isfinite(light).all()
     assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
