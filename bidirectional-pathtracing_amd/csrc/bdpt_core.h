@@ -215,6 +215,9 @@ struct SceneView {
 // Counters for the roofline (algorithmic bytes)
 struct Counters {
   uint32_t nodes, tris, sphs, closest, shadow, hits;
+#ifdef BDPT_PHASE_PROF
+  unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
+#endif
 };
 
 struct Hit {
@@ -298,6 +301,15 @@ namespace bdpt {
 #ifndef BDPT_STACK
 #define BDPT_STACK 64
 #endif
+// Register-stack entries of the megakernel's walk / connection-ray traversals (TravStack<K>).
+// Measured (Lucy stand-in 1080p / CBspheres / CBgems, Msamples/s): K 0: 440 / 438 / 273,
+// K 2: 465 / 452 / 284, K 4: 465 / 450 / 290 (walk 8 or connection 8: no further gain).
+#ifndef BDPT_WALK_STACK
+#define BDPT_WALK_STACK 4
+#endif
+#ifndef BDPT_CONN_STACK
+#define BDPT_CONN_STACK 4
+#endif
 // Children per BVH node: 2 (64-B nodes) or 4 (128-B nodes: half the dependent node fetches per
 // ray, four independent slab tests per fetch). The host emits both trees over the same leaves;
 // a kernel traverses the one its LDS mode selects: scenes fetched from HBM (LM 0, LM 2's nodes below
@@ -317,8 +329,8 @@ BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
-// ones in a private array. K = 0 keeps the whole stack in the array (megakernel: its VGPR budget is
-// spent elsewhere). Near-first traversal of these trees rarely holds more than ~8 entries.
+// ones in a private array (K = 0: all of it). Near-first traversal of these trees rarely holds more
+// than ~8 entries; a few register entries keep most pushes/pops off scratch.
 template <int K>
 struct TravStack {
   int s[K > 0 ? K : 1];
@@ -443,7 +455,9 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
 // other hit children (farther first, so they pop near-first); pop when none is hit.
 // Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
 // Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad
-template <int K, int LM>
+// ORD: visit hit children near-first (closest-hit queries); any-hit queries take them in slot order.
+// A child is entered when its slab interval, clipped to [tmin, tmax], is non-empty.
+template <int K, int LM, bool ORD = true>
 BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
                       Counters& c) {
   constexpr int W = lm_width(LM), NU = node_used_f4(W);
@@ -463,11 +477,11 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     float tnl, tfl, tnr, tfr;
     slab(r, a.x, a.y, a.z, a.w, b.x, b.y, &tnl, &tfl);
     slab(r, b.z, b.w, cc.x, cc.y, cc.z, cc.w, &tnr, &tfr);
-    const bool hl = tnl <= tfl && tnl <= tmax && tfl >= tmin;
-    const bool hr = tnr <= tfr && tnr <= tmax && tfr >= tmin;
+    const bool hl = fmaxf(tnl, tmin) <= fminf(tfl, tmax);
+    const bool hr = fmaxf(tnr, tmin) <= fminf(tfr, tmax);
     const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
     if (hl && hr) {
-      const bool lfirst = tnl <= tnr;
+      const bool lfirst = !ORD || tnl <= tnr;
       stk.push(lfirst ? rref : lref);
       return lfirst ? lref : rref;
     }
@@ -479,20 +493,32 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     const float4 lx = v[0], hx = v[1], ly = v[2 % NU], hy = v[3 % NU];
     const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
     c.nodes += 4;
-    // sort key: entry distance of a hit child, +inf for a miss or an empty slot
-    float k0, k1, k2, k3;
     int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y), r2 = __float_as_int(e.z), r3 = __float_as_int(e.w);
+    float tn0, tn1, tn2, tn3;
+    bool h0, h1, h2, h3;
     {
-      float tn, tf;
-      slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn, &tf);
-      k0 = (r0 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
-      slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn, &tf);
-      k1 = (r1 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
-      slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn, &tf);
-      k2 = (r2 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
-      slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn, &tf);
-      k3 = (r3 != kTravDone && tn <= tf && tn <= tmax && tf >= tmin) ? tn : INFINITY;
+      float tf;
+      slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn0, &tf);
+      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
+      slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn1, &tf);
+      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
+      slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn2, &tf);
+      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
+      slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
+      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
     }
+    if (!ORD) {
+      // continue with the lowest hit slot, push the others
+      int nx = kTravDone;
+      if (h3) nx = r3;
+      if (h2) { if (nx != kTravDone) stk.push(nx); nx = r2; }
+      if (h1) { if (nx != kTravDone) stk.push(nx); nx = r1; }
+      if (h0) { if (nx != kTravDone) stk.push(nx); nx = r0; }
+      if (nx == kTravDone && !stk.pop(nx)) return kTravDone;
+      return nx;
+    }
+    // sort key: entry distance of a hit child, +inf for a miss or an empty slot
+    float k0 = h0 ? tn0 : INFINITY, k1 = h1 ? tn1 : INFINITY, k2 = h2 ? tn2 : INFINITY, k3 = h3 ? tn3 : INFINITY;
     // 5-comparator sorting network on (key, ref)
 #define BDPT_CSWAP(ka, ra, kb, rb)                          \
   {                                                         \
@@ -569,7 +595,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   int ref = S.root;
   c.shadow++;
   for (;;) {
-    while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, tmax, stk, c);
+    while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
     for (int k = 0; k < cnt; k++) {
@@ -624,7 +650,7 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
 template <int LM, int K>
 BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
                                          int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, tmax, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
   if (ref == kTravDone) { *hit = false; return true; }
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -1137,7 +1163,13 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   bool light = false;
   for (;;) {
     Hit h;
-    bool end = !trace_closest<LM>(S, ro, rd, rmin, rmax, h, cnt);
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
+#endif
+    bool end = !trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, rmin, rmax, h, cnt);
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    cnt.clk_walk_trace += __builtin_amdgcn_s_memtime() - tq0;
+#endif
     if (!end) {
       f3 n;
       int mat;

@@ -92,7 +92,7 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
     const float tmax = q.tmax[k];
     vx = q.vx[k]; vy = q.vy[k]; vz = q.vz[k];
     tgt = q.tgt[k];
-    vis = !trace_any<LM>(S, o, d, BDPT_EPS_F, tmax, cnt);
+    vis = !trace_any<LM, BDPT_CONN_STACK>(S, o, d, BDPT_EPS_F, tmax, cnt);
   }
   if (vis && tgt < 0) {
     const int ow = ~tgt;
@@ -406,6 +406,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
     atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
     atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
+    atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
   }
 #endif
   if (STATS) {

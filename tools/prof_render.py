@@ -41,6 +41,8 @@ if os.environ.get("BDPT_PHASES"):
     tot = arr[8] + arr[9] + arr[10]
     print("phase cycles (wave-summed): prepare %.3g (%.1f%%)  conn-gen %.3g (%.1f%%)  flush %.3g (%.1f%%)" % (
         arr[8], 100 * arr[8] / tot, arr[9], 100 * arr[9] / tot, arr[10], 100 * arr[10] / tot))
+    print("  of prepare: walk closest-hit traversal %.1f%% (wave-summed, divergent lanes counted once)" % (
+        100 * arr[11] / max(1, arr[8])))
 if os.environ.get("BDPT_STATS") == "1":
     st = pt.stats()
     n = max(1, st.samples)
