@@ -63,6 +63,41 @@ def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0) -> dict
                       f"(reference arithmetic) with {threads} threads, {t_tot:.1f} s"}
 
 
+REF_DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
+
+
+def cpu_baseline_reference(dae: str, name: str, threads: int, budget_s: float = 15.0):
+    """The reference's own `-t N` CPU path: oracle/_ref/ref_driver (built by __graft_entry__.build()
+    from the reference's sources: RaytracedRenderer + BidirectionalPathTracer, reference flags)
+    rendering the same scene and resolution at a few spp. Render seconds are the reference's own
+    "Rendering... 100%! (Xs)" report (tiles + its per-tile frame tonemap, excluding parse/BVH
+    build). None when the binary is not present."""
+    import re
+    import subprocess
+    import tempfile
+    if not os.path.exists(REF_DRIVER) or not os.path.exists(dae):
+        return None
+    done, t_tot, spp_run, runs = 0, 0.0, 1, 0
+    with tempfile.TemporaryDirectory() as td:
+        while t_tot < budget_s * 0.6 and runs < 3:
+            r = subprocess.run([REF_DRIVER, "-s", str(spp_run), "-t", str(threads), "-m", str(M), "-r", str(W),
+                                str(H), "-f", os.path.join(td, "ref.png"), dae], capture_output=True,
+                               text=True, timeout=600, cwd=td)
+            m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", r.stdout)
+            if r.returncode != 0 or not m:
+                return None
+            dt = float(m[-1])
+            t_tot += dt
+            done += W * H * spp_run
+            runs += 1
+            rate = W * H * spp_run / dt
+            spp_run = max(1, int((budget_s - t_tot) * rate / (W * H)))
+    return {"value": done / t_tot / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
+            "sample": f"{name} {W}x{H}, {done // (W * H)} spp, m={M}: the reference's RaytracedRenderer + "
+                      f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2) at -t {threads}, "
+                      f"{t_tot:.1f} s of rendering"}
+
+
 def parity_check(scene, seed: int) -> dict:
     """Per-pixel RMSE of the GPU sample buffer vs the oracle's COUNTER32 CPU path, same seed,
     same workload at 2 spp (the CPU side of the metric)."""
@@ -218,7 +253,13 @@ def main() -> int:
     if world == 1 and not args.no_parity:
         out["parity"] = parity_check(scene, seed)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, args.scene, threads=min(16, os.cpu_count() or 1))
+        thr = min(16, os.cpu_count() or 1)
+        dae = args.scene if args.scene.endswith(".dae") else os.path.join(REPO, "scenes", args.scene + ".dae")
+        port = cpu_baseline(scene, args.scene, threads=thr)
+        ref = cpu_baseline_reference(dae, os.path.basename(args.scene), threads=thr)
+        out["cpu_baseline"] = ref if ref is not None else port
+        if ref is not None:   # the oracle port's fp64 path, same host, for comparison
+            out["cpu_baseline"]["port"] = {"value": port["value"], "cores": port["cores"], "sample": port["sample"]}
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -337,6 +337,7 @@ struct TravStack {
   int nreg, msp;
   int* mem;   // a separate private array, so that s[] / nreg / msp stay in registers
   BDPT_HD explicit TravStack(int* m) : nreg(0), msp(0), mem(m) {}
+  BDPT_HD void clear() { nreg = 0; msp = 0; }
   BDPT_HD void push(int v) {
     if (K == 0) {
       mem[msp++] = v;

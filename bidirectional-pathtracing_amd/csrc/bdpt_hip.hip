@@ -191,7 +191,7 @@ __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int h
   float tmax = 0;
   RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
   int stack_mem[BDPT_STACK];
-  TravStack<0> stk(stack_mem);
+  TravStack<BDPT_CONN_STACK> stk(stack_mem);
   for (;;) {
     const unsigned long long idle = __ballot(!active);
     const int take = min(__popcll(idle), tail - next);
@@ -204,7 +204,7 @@ __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int h
         tmax = q.tmax[k];
         r = make_rayinv(o, d);
         ref = S.root;
-        stk.msp = 0;
+        stk.clear();
         cnt.shadow++;
         active = true;
       }
@@ -213,7 +213,7 @@ __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int h
     if (__ballot(active) == 0) break;
     for (;;) {
       bool hit = false;
-      if (active && any_step<LM, 0>(S, r, o, d, BDPT_EPS_F, tmax, ref, stk, &hit, cnt)) {
+      if (active && any_step<LM, BDPT_CONN_STACK>(S, r, o, d, BDPT_EPS_F, tmax, ref, stk, &hit, cnt)) {
         active = false;
         if (!hit) {
           const int tgt = q.tgt[k];

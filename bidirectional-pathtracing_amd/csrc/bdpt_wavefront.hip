@@ -682,7 +682,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_rf(WfParams p) {
       h.t = b.w; h.prim = -1; h.key = -1; h.b1 = 0; h.b2 = 0;
       ref = p.S.root;
       stk.nreg = 0;
-      stk.msp = 0;
+      stk.clear();
       cnt.closest++;
       active = true;
     }
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_shadow_rf(WfParams p) {
       r = make_rayinv(o, d);
       ref = p.S.root;
       stk.nreg = 0;
-      stk.msp = 0;
+      stk.clear();
       cnt.shadow++;
       active = true;
     }
