@@ -52,18 +52,24 @@ class Camera(C.Structure):
                 ("fclip", C.c_double)]
 
 
+class EnvMapDesc(C.Structure):
+    """bdpt_envmap: the -e environment map (HDRImageBuffer data[w*j + i], row 0 = theta 0)."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.POINTER(C.c_float))]
+
+
 class SceneDesc(C.Structure):
     _fields_ = [("nprim", C.c_int32), ("prim_type", C.POINTER(C.c_int32)),
                 ("prim_geom", C.POINTER(C.c_double)), ("prim_mat", C.POINTER(C.c_int32)),
                 ("nmat", C.c_int32), ("mats", C.POINTER(Material)),
-                ("nlight", C.c_int32), ("lights", C.POINTER(Light)), ("camera", Camera)]
+                ("nlight", C.c_int32), ("lights", C.POINTER(Light)), ("camera", Camera),
+                ("envmap", C.POINTER(EnvMapDesc))]
 
 
 class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
                 ("max_depth", C.c_int32), ("seed", C.c_uint64), ("samples_per_lane", C.c_int32),
                 ("device", C.c_int32), ("collect_stats", C.c_int32), ("pipeline", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("russian_roulette", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class Tile(C.Structure):
@@ -85,7 +91,7 @@ class Scene:
     """Owns numpy arrays backing a SceneDesc (keeps them alive while the desc is used)."""
 
     def __init__(self, prim_type, prim_geom, prim_mat, mats, lights, camera: dict,
-                 width: int = 0, height: int = 0):
+                 width: int = 0, height: int = 0, envmap: Optional[np.ndarray] = None):
         self.prim_type = np.ascontiguousarray(prim_type, dtype=np.int32)
         self.prim_geom = np.ascontiguousarray(prim_geom, dtype=np.float64).reshape(-1, 18)
         self.prim_mat = np.ascontiguousarray(prim_mat, dtype=np.int32)
@@ -99,6 +105,20 @@ class Scene:
         self.nlight = len(lights)
         self.camera = camera
         self.width, self.height = width, height
+        self.set_envmap(envmap)
+
+    def set_envmap(self, envmap: Optional[np.ndarray]) -> None:
+        """Environment map (H, W, 3) float32, row 0 = theta 0 (+y); None removes it."""
+        if envmap is None:
+            self.envmap = None
+            self._env_desc = None
+            return
+        self.envmap = np.ascontiguousarray(envmap, dtype=np.float32).reshape(
+            envmap.shape[0], envmap.shape[1], 3)
+        e = EnvMapDesc()
+        e.height, e.width = self.envmap.shape[0], self.envmap.shape[1]
+        e.rgb = self.envmap.ctypes.data_as(C.POINTER(C.c_float))
+        self._env_desc = e
 
     @property
     def nprim(self) -> int:
@@ -122,6 +142,7 @@ class Scene:
         cam.hfov_deg, cam.vfov_deg = c["hFov"], c["vFov"]
         cam.nclip, cam.fclip = c["nClip"], c["fClip"]
         d.camera = cam
+        d.envmap = C.pointer(self._env_desc) if self._env_desc is not None else None
         return d
 
 
@@ -221,8 +242,21 @@ def retarget_camera(scene: Scene, width: int, height: int) -> Scene:
     c["screenW"], c["screenH"] = width, height
     out = Scene(scene.prim_type, scene.prim_geom, scene.prim_mat,
                 [scene.mats[i] for i in range(scene.nmat)],
-                [scene.lights[i] for i in range(scene.nlight)], c, width, height)
+                [scene.lights[i] for i in range(scene.nlight)], c, width, height, scene.envmap)
     return out
+
+
+def load_exr(path: str) -> np.ndarray:
+    """OpenEXR environment map through the library's reader (bdpt_exr_load: load_exr,
+    main.cpp:40-77): (H, W, 3) float32, row 0 = top."""
+    lib = load_library()
+    w, h = C.c_int32(), C.c_int32()
+    ptr = C.POINTER(C.c_float)()
+    _check(lib.bdpt_exr_load(os.fsencode(path), C.byref(w), C.byref(h), C.byref(ptr)), lib)
+    try:
+        return np.ctypeslib.as_array(ptr, shape=(h.value, w.value, 3)).copy()
+    finally:
+        lib.bdpt_exr_free(ptr)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -258,6 +292,10 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_dae_dump_json.argtypes = [C.c_void_p, C.c_char_p]
     lib.bdpt_dae_free.argtypes = [C.c_void_p]
     lib.bdpt_dae_free.restype = None
+    lib.bdpt_exr_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                  C.POINTER(C.POINTER(C.c_float))]
+    lib.bdpt_exr_free.argtypes = [C.POINTER(C.c_float)]
+    lib.bdpt_exr_free.restype = None
     if path is None:
         _lib = lib
     return lib
@@ -279,7 +317,8 @@ class BidirectionalPathTracer:
 
     def __init__(self, scene: Scene, width: int, height: int, spp: int, max_depth: int,
                  seed: int = 5489, device: int = 0, samples_per_lane: int = 0,
-                 collect_stats: bool = False, pipeline: int = PIPELINE_AUTO):
+                 collect_stats: bool = False, pipeline: int = PIPELINE_AUTO,
+                 russian_roulette: bool = False):
         self.lib = load_library()
         self.scene = scene
         self.width, self.height, self.spp, self.max_depth = width, height, spp, max_depth
@@ -288,6 +327,7 @@ class BidirectionalPathTracer:
         p.seed, p.samples_per_lane, p.device = seed, samples_per_lane, device
         p.collect_stats = 1 if collect_stats else 0
         p.pipeline = pipeline
+        p.russian_roulette = 1 if russian_roulette else 0
         self._desc = scene.desc()
         ctx = C.c_void_p()
         _check(self.lib.bdpt_create(C.byref(self._desc), C.byref(p), C.byref(ctx)), self.lib)

@@ -166,10 +166,41 @@ BDPT_HD void cos_sin_2pi(float u, float* c, float* s) {
   *s = ss;
 }
 
+// atan2(y, x) for the environment map's direction -> (theta, phi) (environment_light.cpp:97-102):
+// octant reduction + the Cephes atanf polynomial (|err| ~ 1e-7), plain fp32 operations so the
+// oracle's mode 2 (oracle/bdpt_oracle.cpp atan2_f32) evaluates it bit-identically.
+BDPT_HD float atan2_det(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  if (ax == 0.0f && ay == 0.0f) return 0.0f;
+  float t = ay <= ax ? ay / ax : ax / ay;   // [0, 1]
+  float off = 0.0f;
+  if (t > 0.41421356237309503f) {           // tan(pi/8): atan t = pi/4 + atan((t-1)/(t+1))
+    off = 0.78539816339744831f;
+    t = (t - 1.0f) / (t + 1.0f);
+  }
+  const float z = t * t;
+  float r = ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z) * t + t;
+  r = off + r;
+  if (ay > ax) r = 1.57079632679489662f - r;
+  if (x < 0.0f) r = 3.14159265358979323f - r;
+  return y < 0.0f ? -r : r;
+}
+// lround for x >= 0 (std::lround: halves away from zero), exact: x - floor(x) is exact.
+BDPT_HD int lround_pos(float x) {
+  const float f = floorf(x);
+  return (int)f + ((x - f) >= 0.5f ? 1 : 0);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Scene layout in HBM (see DESIGN.md §Data layout)
 enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REFRACTION = 4 };
-enum { LIGHT_AREA = 0, LIGHT_POINT = 1 };
+// Vtx::mat of a vertex without BSDF: -1 camera / area or point light vertex, MAT_ENV_V a vertex
+// of the environment light (an escaped eye ray, or an env light subpath's first vertex).
+enum { MAT_ENV_V = -2 };
+enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2 };
+// Russian roulette (bdpt_params.russian_roulette): vertices with index i > BDPT_RR_MIN continue
+// with p_keep = min(1, |f| / pdf) (the rule commented out at bidirection.cpp:87-93).
+#define BDPT_RR_MIN 3
 
 struct DMat {
   int type;
@@ -180,8 +211,21 @@ struct DMat {
 struct DLight {
   int type;
   float rad[3], pos[3], dir[3], dx[3], dy[3];
-  float area;
+  float area;                 // LIGHT_ENV: pi R^2 of the scene's bounding sphere (emission disk)
   float fx[3], fy[3], fz[3];  // make_coord_space(dir)
+};
+
+// Environment light (EnvironmentLight, environment_light.cpp): the map and its sampling tables
+// (init(), :18-62) built in fp64 on the host and rounded to fp32, plus the scene's bounding
+// sphere that sample_Le emits from.
+struct EnvView {
+  const float* marg;   // h: marginal_y (CDF over rows)
+  const float* cond;   // w*h: conds_y (per-row CDFs)
+  const float* pdf;    // w*h: pdf_envmap
+  const float* rgb;    // w*h*3: data[w*j + i]
+  int w, h;
+  int light;           // index of the env light in the light list (-1: none)
+  float cx, cy, cz, rad;
 };
 struct DCam {
   float pos[3];
@@ -209,6 +253,7 @@ struct SceneView {
   const float4* lgeom;   // LDS copy of the geometry (LM 1 only)
   int ntop;
   DCam cam;
+  EnvView env;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -801,20 +846,105 @@ BDPT_HD float pdf_b(const DMat& M, f3 n, f3 zh, f3 dw) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
+// EnvironmentLight (environment_light.cpp) in the device semantics: w points from the scene toward
+// the environment (sample_L's *wi, sample_dir's r.d).
+BDPT_HD int upper_idx(const float* a, int n, float u) {   // std::upper_bound(a, a + n, u) - a, <= n - 1
+  int lo = 0, cnt = n;
+  while (cnt > 0) {
+    const int st = cnt >> 1, m = lo + st;
+    if (!(u < a[m])) { lo = m + 1; cnt -= st + 1; }
+    else cnt = st;
+  }
+  return lo < n ? lo : n - 1;
+}
+BDPT_HD f3 env_texel(const EnvView& E, int k) {
+  const float* p = E.rgb + 3 * (size_t)k;
+  return mk3(p[0], p[1], p[2]);
+}
+BDPT_HD f3 env_bilerp(const EnvView& E, float x, float y) {   // bilerp (:106-123)
+  int right = lround_pos(x), left, v = lround_pos(y);
+  const float u1 = ((float)right - x) + 0.5f;
+  float v1;
+  if (right == 0 || right == E.w) { left = E.w - 1; right = 0; }
+  else left = right - 1;
+  if (v == 0) { v = 1; v1 = 1.0f; }
+  else if (v == E.h) { v = E.h - 1; v1 = 0.0f; }
+  else v1 = ((float)v - y) + 0.5f;
+  const int bottom = E.w * v, top = bottom - E.w;
+  const float u0 = 1 - u1;
+  const f3 a = add(muls(env_texel(E, top + left), u1), muls(env_texel(E, top + right), u0));
+  const f3 b = add(muls(env_texel(E, bottom + left), u1), muls(env_texel(E, bottom + right), u0));
+  return add(muls(a, v1), muls(b, 1 - v1));
+}
+// theta_phi_to_dir(xy_to_theta_phi(x, y)) (:88-104): phi = 2 pi x / w, theta = pi y / h;
+// (cos(phi - pi) sin t, cos t, -sin(phi - pi) sin t) = (-cos phi sin t, cos t, sin phi sin t).
+BDPT_HD f3 env_xy_to_dir(const EnvView& E, float x, float y, float* sin_theta) {
+  float cp, sp, ct, st;
+  cos_sin_2pi(x / (float)E.w, &cp, &sp);
+  cos_sin_2pi((y / (float)E.h) * 0.5f, &ct, &st);
+  *sin_theta = st;
+  return mk3(-cp * st, ct, sp * st);
+}
+// theta_phi_to_xy(dir_to_theta_phi(u)) (:81-86, 97-102) for a unit u: theta = acos(u.y),
+// phi = atan2(-u.z, u.x) + pi; sin(theta) as sqrt((1 - y)(1 + y)).
+BDPT_HD void env_dir_to_xy(const EnvView& E, f3 u, float* x, float* y, float* sin_theta) {
+  const float st = sqrtf(fmaxf(0.0f, (1.0f - u.y) * (1.0f + u.y)));
+  const float th = atan2_det(st, u.y);
+  const float ph = atan2_det(-u.z, u.x) + BDPT_PI_F;
+  *x = ph / 2.0f / BDPT_PI_F * (float)E.w;
+  *y = th / BDPT_PI_F * (float)E.h;
+  *sin_theta = st;
+}
+// sample_dir (:159-168): the radiance arriving along -u from direction u
+BDPT_HD f3 env_radiance(const EnvView& E, f3 u) {
+  float x, y, st;
+  env_dir_to_xy(E, u, &x, &y, &st);
+  return env_bilerp(E, x, y);
+}
+// Solid-angle density of sample_L choosing direction u (the pdf sample_L returns, :152, for the
+// texel u falls in); 0 at the poles.
+BDPT_HD float env_pdf_dir(const EnvView& E, f3 u) {
+  float x, y, st;
+  env_dir_to_xy(E, u, &x, &y, &st);
+  if (!(st > 0.0f)) return 0.0f;
+  const int xi = (int)x, yi = (int)y;
+  const int i = xi < E.w - 1 ? xi : E.w - 1, j = yi < E.h - 1 ? yi : E.h - 1;
+  return E.pdf[E.w * j + i] * (float)(E.w * E.h) / (2.0f * BDPT_PI_F * BDPT_PI_F * st);
+}
+// sample_L's direction sampling (:126-156): row by the marginal CDF, column by the row's CDF, then
+// a uniform jitter inside the texel; returns bilerp(xy) (4 uniforms).
+BDPT_HD f3 env_sample_dir(const EnvView& E, Rng& g, f3* w, float* pdf) {
+  float ux, uy;
+  grid2d(g, &ux, &uy);
+  const int y = upper_idx(E.marg, E.h, uy);
+  const int x = upper_idx(E.cond + (size_t)E.w * y, E.w, ux);
+  const float xf = (float)x + rng_next(g);
+  const float yf = (float)y + rng_next(g);
+  float st;
+  *w = env_xy_to_dir(E, xf, yf, &st);
+  *pdf = E.pdf[E.w * y + x] * (float)(E.w * E.h) / (2.0f * BDPT_PI_F * BDPT_PI_F * st);
+  return env_bilerp(E, xf, yf);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Path vertices (PathVertex, bidirection.h:29-46) with the MIS path constants attached.
 struct Vtx {
   f3 pos, n, zh, alpha;
   float fwd;   // MIS denominator of the step at this vertex (bidirection.cpp:194-211 / 257-280)
-  float gp;    // MIS prefix: G of the vertex one step inward (see mis_horner), 0 at E[2] / L[1]
-  int mat;     // -1: no BSDF (camera / light vertex)
-  int conn;    // can receive a connection: diffuse (the only BSDF with f != 0, bsdf.cpp:52-62),
-               // seen from its front side (wo.z >= 0 toward the previous vertex), alpha != 0
+  float gp;    // MIS prefix: G of the vertex one step inward (see mis_horner), 0 at E[2] / L[1];
+               // during the walk it holds the vertex's roulette probability q (PathVertex.q)
+               // until the *_constants pass has consumed it
+  int mat;     // -1: no BSDF (camera / light vertex); MAT_ENV_V: environment vertex
+  float cq;    // > 0: can receive a connection — diffuse (the only BSDF with f != 0,
+               // bsdf.cpp:52-62), seen from its front side (wo.z >= 0 toward the previous vertex),
+               // alpha != 0 — and then equal to q; 0: cannot
 };
 
 struct LightSample {
   f3 pos, n, zh, alpha;
   float dir_pdf;
+  float fwd;   // point_pdf / nL (the MIS denominator of the light end in environment scenes)
+  bool env;    // environment light: n = zh = -w, pos unused
 };
 
 template <int MAXV>
@@ -829,6 +959,7 @@ struct Paths {
 struct SampleParams {
   int W, H, spp, max_depth;
   uint64_t seed;
+  int rr;   // Russian roulette (bdpt_params.russian_roulette; honoured by EXT kernels only)
 };
 
 // Power-heuristic sums in Horner form. Along a subpath walked from the connection endpoint
@@ -853,24 +984,36 @@ BDPT_HD float step_g(f3 cur_pos, f3 cur_n, f3 oth_pos, f3 oth_zh, f3* dw_out) {
   *dw_out = dw;
   return fabsf(wz * dot(dw, cur_n)) / (dist * dist);
 }
+// The same with environment vertices: an env vertex sits at infinity in direction
+// w, with n = zh = -w. oth env: d = -w and g = |dot(d, cur.n)| (the emission disk's planar density
+// projected onto cur); cur env: d = w and g = 1 (densities of an env vertex are solid-angle ones).
+BDPT_HD float step_gx(f3 cur_pos, f3 cur_n, bool cur_env, f3 oth_pos, f3 oth_zh, bool oth_env, f3* dw_out) {
+  if (cur_env) { *dw_out = neg(cur_n); return 1.0f; }
+  if (oth_env) { *dw_out = oth_zh; return fabsf(dot(oth_zh, cur_n)); }
+  return step_g(cur_pos, cur_n, oth_pos, oth_zh, dw_out);
+}
+BDPT_HD bool is_env(const Vtx& v) { return v.mat == MAT_ENV_V; }
 
-// Per-subpath MIS constants (see Vtx).
-template <int MAXV>
+// Per-subpath MIS constants (see Vtx). EXT: the scene has an environment light or the walks use
+// Russian roulette (q = Vtx::gp on entry); EXT = false compiles to the reference-only path.
+template <int MAXV, bool EXT = false>
 BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   int nh = P.nE - 2;
   for (int k = 0; k < nh; k++) {   // vertex E[k+2]
     Vtx& v = P.E[k];
+    const bool venv = EXT && is_env(v);
     f3 prevp = k == 0 ? cam : P.E[k - 1].pos;
-    v.conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(prevp, v.pos)), v.zh) >= 0 &&
-             nonzero3(v.alpha);
+    const bool conn = !venv && S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(prevp, v.pos)), v.zh) >= 0 &&
+                      nonzero3(v.alpha);
+    v.cq = conn ? (EXT ? v.gp : 1.0f) : 0.0f;
     if (k == 0) {
       v.fwd = 1.0f * 1.0f;
     } else {
       const Vtx& nx = P.E[k - 1];
       f3 dw;
-      float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
-      float p = pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
+      float g2 = EXT ? step_gx(v.pos, v.n, venv, nx.pos, nx.zh, false, &dw) : step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
+      float p = pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * (EXT ? nx.gp : 1.0f);
       v.fwd = p * g2;
     }
   }
@@ -880,30 +1023,37 @@ BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
     v.gp = G;
     if (k + 1 < nh) {
       const Vtx& pv = P.E[k + 1];
-      f3 dw;
-      float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
-      G = mis_horner((p * g) / v.fwd, !((P.dE >> (k + 1)) & 3u), G);
+      if (EXT && is_env(pv)) {
+        G = 0.0f;   // an escaped vertex ends the path; the j = 0 weight recomputes this step
+      } else {
+        f3 dw;
+        float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+        float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * (EXT ? pv.gp : 1.0f);
+        G = mis_horner((p * g) / v.fwd, !((P.dE >> (k + 1)) & 3u), G);
+      }
     }
   }
 }
 
-template <int MAXV>
+template <int MAXV, bool EXT = false>
 BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
   int nv = P.nL - 1;   // L[1..nL-1]
+  const bool l1env = EXT && is_env(P.L[0]);
   for (int k = 0; k < nv; k++) {   // vertex L[k+1]
     Vtx& v = P.L[k];
     if (k == 0) {
       v.fwd = l1_p;
-      v.conn = 0;
+      v.cq = 0.0f;
       continue;
     }
     const Vtx& nx = P.L[k - 1];
-    v.conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(nx.pos, v.pos)), v.zh) >= 0 &&
-             nonzero3(v.alpha);
+    const bool conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(nx.pos, v.pos)), v.zh) >= 0 &&
+                      nonzero3(v.alpha);
+    v.cq = conn ? (EXT ? v.gp : 1.0f) : 0.0f;
     f3 dw;
-    float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
-    float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * 1.0f;
+    float g2 = EXT ? step_gx(v.pos, v.n, false, nx.pos, nx.zh, k == 1 && l1env, &dw)
+                   : step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
+    float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * (EXT ? nx.gp : 1.0f);
     v.fwd = p * g2;
   }
   float G = 0.0f;
@@ -913,8 +1063,9 @@ BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
     if (k + 1 < nv) {
       const Vtx& pv = P.L[k + 1];
       f3 dw;
-      float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * 1.0f;
+      float g = EXT ? step_gx(v.pos, v.n, k == 0 && l1env, pv.pos, pv.zh, false, &dw)
+                    : step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
+      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * (EXT ? pv.gp : 1.0f);
       G = mis_horner((p * g) / v.fwd, !((P.dL >> k) & 3u), G);
     }
   }
@@ -930,6 +1081,7 @@ BDPT_HD bool light_contains(const DLight& l, f3 p) {
 // sample_pdf's dir_pdf for a point known to be on the light; wi = direction of travel.
 BDPT_HD float light_dir_pdf(const DLight& l, f3 wi) {
   if (l.type == LIGHT_POINT) return 0.25f / BDPT_PI_F;
+  if (l.type == LIGHT_ENV) return 1.0f / l.area;   // planar density of the emission disk (§9)
   Frame f;
   f.X = mk3(l.fx[0], l.fx[1], l.fx[2]);
   f.Y = mk3(l.fy[0], l.fy[1], l.fy[2]);
@@ -971,7 +1123,27 @@ BDPT_HD LightSample light_sample_point(const DLight& l, int nlights, Rng& g, f3 
   lpp = lpp / (float)nlights;
   s.alpha = divs(rad, lpp);
   s.zh = zaxis(s.n);
+  s.fwd = lpp;
+  s.env = false;
   *lpp_out = lpp;
+  return s;
+}
+// sample_Le_point of the environment light: a direction w from sample_L's
+// importance sampling; point_pdf = its solid-angle pdf / nL, dir_pdf = the emission disk's planar
+// density 1/(pi R^2); the vertex sits at infinity (n = zh = -w).
+BDPT_HD LightSample env_sample_point(const SceneView& S, Rng& g, f3 p) {
+  LightSample s;
+  f3 w;
+  float pw;
+  const f3 rad = env_sample_dir(S.env, g, &w, &pw);
+  const float lpp = pw / (float)S.nlights;
+  s.pos = p;
+  s.n = neg(w);
+  s.zh = s.n;
+  s.dir_pdf = 1.0f / S.lights[S.env.light].area;
+  s.alpha = divs(rad, lpp);
+  s.fwd = lpp;
+  s.env = true;
   return s;
 }
 
@@ -1025,7 +1197,7 @@ BDPT_HD EyeSample camera_sample(const DCam& c, int W, int H, f3 p) {
 // i, j: reference vertex indices; ls: fresh light sample (j == 1); es: camera sample (i == 1);
 // dc, dist: normalize(vl - ve) and |vl - ve| of the connection (j >= 1), which are exactly the
 // endpoint-step directions the reference recomputes (normalize(-v) == -normalize(v) in IEEE).
-template <class PA>
+template <bool EXT = false, class PA>
 BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const Vtx* lv, int i, int j,
                          const LightSample& ls, const EyeSample& es, int eye_light, f3 dc, float dist) {
 #ifdef BDPT_EXP_NOMIS
@@ -1034,42 +1206,60 @@ BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const V
   float ge = 0.0f, gl = 0.0f;
   if (i >= 2) {
     const Vtx& cur = *ev;
+    const bool cenv = EXT && is_env(cur);
     float nom;
     if (j == 0) {
-      float p = S.lights[eye_light].type == LIGHT_POINT ? 1.0f : 1.0f / S.lights[eye_light].area;
+      const DLight& EL = S.lights[eye_light];
+      float p = EL.type == LIGHT_POINT ? 1.0f
+                : (EXT && EL.type == LIGHT_ENV) ? env_pdf_dir(S.env, neg(cur.n)) / (float)S.nlights
+                                                : 1.0f / EL.area;
       nom = p * 1.0f;
     } else {
       f3 pzh = j == 1 ? ls.zh : lv->zh;
       f3 dw = neg(dc);   // normalize(E[i] - vl)
-      float g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
-      float p = j == 1 ? ls.dir_pdf * 1.0f : pdf_b(S.mats[lv->mat], lv->n, pzh, dw) * 1.0f;
+      float g = (EXT && j == 1 && ls.env) ? fabsf(dot(dw, cur.n))
+                                          : fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
+      float p = j == 1 ? ls.dir_pdf * 1.0f : pdf_b(S.mats[lv->mat], lv->n, pzh, dw) * (EXT ? lv->cq : 1.0f);
       nom = p * g;
     }
     float below = cur.gp;   // G_{i-1}
     if (j == 0 && i >= 3) {  // the step below the emitter uses the light's dir_pdf (:224-232)
       const Vtx v = P.e(i - 1);
       f3 dr;
-      const float revg = step_g(v.pos, v.n, cur.pos, cur.zh, &dr);   // g of the step E[i-1] <- E[i]
-      f3 dw = normalize(sub(v.pos, cur.pos));
+      const float revg = EXT ? step_gx(v.pos, v.n, false, cur.pos, cur.zh, cenv, &dr)
+                             : step_g(v.pos, v.n, cur.pos, cur.zh, &dr);   // g of the step E[i-1] <- E[i]
+      f3 dw = cenv ? cur.n : normalize(sub(v.pos, cur.pos));
       float dp = light_dir_pdf(S.lights[eye_light], neg(dw));
       below = mis_horner(((dp * 1.0f) * revg) / v.fwd, !((P.dE >> (i - 2)) & 3u), v.gp);
     }
-    ge = mis_horner(nom / cur.fwd, !((P.dE >> (i - 1)) & 3u), below);   // delta(E[i]) || delta(E[i-1])
+    // delta(E[i]) || delta(E[i-1]); an escaped camera ray (i = 2) has no camera-connection strategy
+    const bool t = !((P.dE >> (i - 1)) & 3u) && !(cenv && i == 2);
+    ge = mis_horner(nom / cur.fwd, t, below);
   }
   if (j >= 1) {
-    const Vtx& cur = *lv;   // j == 1: the original L[1], not the fresh sample (quirk 5)
-    f3 pzh = i == 1 ? es.zh : ev->zh;
-    f3 dw;
-    float g;
-    if (j >= 2) {   // cur = L[j] = vl: normalize(L[j] - ve) = dc
-      dw = dc;
-      g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
+    if (EXT && j == 1 && S.env.light >= 0) {
+      // environment scenes: the light end of (i, 1) is the fresh sample itself
+      f3 dw;
+      float g;
+      if (ls.env) { dw = dc; g = 1.0f; }
+      else g = step_g(ls.pos, ls.n, i == 1 ? es.pos : ev->pos, i == 1 ? es.zh : ev->zh, &dw);
+      float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[ev->mat], ev->n, ev->zh, dw) * ev->cq;
+      gl = mis_horner((p * g) / ls.fwd, true, 0.0f);
     } else {
-      f3 ppos = i == 1 ? es.pos : ev->pos;
-      g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+      const Vtx& cur = *lv;   // j == 1: the original L[1], not the fresh sample (quirk 5)
+      f3 pzh = i == 1 ? es.zh : ev->zh;
+      f3 dw;
+      float g;
+      if (j >= 2) {   // cur = L[j] = vl: normalize(L[j] - ve) = dc
+        dw = dc;
+        g = fabsf(lz(dw, pzh) * dot(dw, cur.n)) / (dist * dist);
+      } else {
+        f3 ppos = i == 1 ? es.pos : ev->pos;
+        g = step_g(cur.pos, cur.n, ppos, pzh, &dw);
+      }
+      float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[ev->mat], ev->n, pzh, dw) * (EXT ? ev->cq : 1.0f);
+      gl = mis_horner((p * g) / cur.fwd, !((P.dL >> (j - 1)) & 3u), cur.gp);
     }
-    float p = i <= 1 ? es.dir_pdf * 1.0f : pdf_b(S.mats[ev->mat], ev->n, pzh, dw) * 1.0f;
-    gl = mis_horner((p * g) / cur.fwd, !((P.dL >> (j - 1)) & 3u), cur.gp);
   }
   return 1.0f / ((1.0f + ge) + gl);
 }
@@ -1090,7 +1280,7 @@ struct PathsInRegs {
 // eye walk ends starts its light walk in the next iteration, so a wave iterates
 // max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
 // sample + walk: 1) make the interleaving invisible in the results.
-template <int MAXV, int LM = 0>
+template <int MAXV, int LM = 0, bool EXT = false>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
   rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
@@ -1104,8 +1294,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le, on stream 1
   f3 lo, ld, ln;
   float lpp, ldp;
+  float mis_p, mis_dir;   // L[1]'s MIS densities (differ from lpp / ldp only for the env light)
   f3 lrad;
   uint32_t lpos;
+  bool l1env = false;
   {
     Rng gl = g;
     rng_stream(gl, 1);
@@ -1113,7 +1305,26 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     if (lid >= S.nlights) lid = S.nlights - 1;
     const DLight& L0 = S.lights[lid];
     lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
-    if (L0.type == LIGHT_POINT) {
+    if (EXT && L0.type == LIGHT_ENV) {
+      // sample_Le of the environment light: direction by sample_L's importance
+      // sampling, origin uniform on the disk of radius R facing -w, tangent to the bounding sphere
+      f3 w;
+      float pw;
+      lrad = env_sample_dir(S.env, gl, &w, &pw);
+      const float u1 = rng_next(gl), u2 = rng_next(gl);
+      const float r = S.env.rad * sqrtf(u1);
+      float c, sn;
+      cos_sin_2pi(u2, &c, &sn);
+      const Frame wf = make_frame(w);
+      lo = add(add(add(mk3(S.env.cx, S.env.cy, S.env.cz), smul(S.env.rad, w)), smul(r * c, wf.X)), smul(r * sn, wf.Y));
+      ld = neg(w);
+      ln = ld;
+      lpp = 1.0f / L0.area;
+      ldp = pw;
+      mis_p = pw;
+      mis_dir = 1.0f / L0.area;
+      l1env = true;
+    } else if (L0.type == LIGHT_POINT) {
       float z = rng_next(gl) * 2 - 1;
       float sinT = sqrtf(fmaxf(0.0f, 1.0f - z * z));
       float u = rng_next(gl);
@@ -1124,6 +1335,8 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       lpp = 1;
       ldp = 0.25f / BDPT_PI_F;
       ln = ld;
+      mis_p = lpp;
+      mis_dir = ldp;
     } else {
       float sx, sy;
       grid2d(gl, &sx, &sy);
@@ -1139,20 +1352,23 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       ld = to_world(lf, dl);
       lpp = 1.0f / L0.area;
       ln = mk3(L0.dir[0], L0.dir[1], L0.dir[2]);
+      mis_p = lpp;
+      mis_dir = ldp;
     }
     lpos = gl.pos;
   }
   lpp = lpp / (float)S.nlights;
+  mis_p = mis_p / (float)S.nlights;
   {
     Vtx& v1 = P.L[0];
     v1.pos = lo;
     v1.n = ln;
-    v1.zh = zaxis(ln);
+    v1.zh = l1env ? ln : zaxis(ln);
     v1.alpha = divs(lrad, lpp);
-    v1.mat = -1;
-    v1.gp = 0; v1.conn = 0;
+    v1.mat = l1env ? (int)MAT_ENV_V : -1;
+    v1.gp = 0; v1.cq = 0;
   }
-  P.l1_dir_pdf = ldp;
+  P.l1_dir_pdf = mis_dir;
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
   f3 ro = cam;
   float rmin = S.cam.nclip, rmax = S.cam.fclip;
@@ -1171,6 +1387,17 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     cnt.clk_walk_trace += __builtin_amdgcn_s_memtime() - tq0;
 #endif
+    if (EXT && end && !light && S.env.light >= 0) {
+      // an escaped eye ray ends on the environment light: vertex at infinity in direction rd
+      Vtx v;
+      v.alpha = divs(mul(muls(prev_alpha, fabsf(dot(prev_n, rd))), prev_f), prev_pdf);
+      v.pos = ro;
+      v.n = neg(rd);
+      v.zh = v.n;
+      v.mat = MAT_ENV_V;
+      v.fwd = 1; v.gp = 1; v.cq = 0;
+      P.E[count++] = v;
+    }
     if (!end) {
       f3 n;
       int mat;
@@ -1184,8 +1411,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.n = n;
       v.zh = fr.Z;
       v.mat = mat;
-      v.fwd = 1; v.gp = 0; v.conn = 0;
-      (light ? P.L + 1 : P.E)[count++] = v;
+      v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
+      Vtx* slot = (light ? P.L + 1 : P.E) + count++;
+      *slot = v;
       if (is_delta(M.type)) dm |= 1u << i;
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
@@ -1193,13 +1421,20 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         f3 wi;
         float pdf;
         const f3 fv = sample_f(M, g, to_local(fr, neg(rd)), &wi, &pdf);
+        float q = 1.0f;
+        if (EXT && sp.rr && i > BDPT_RR_MIN) {
+          // p_keep = min(1, |f| / pdf), PathVertex.q, then coin_flip(p_keep) (bidirection.cpp:87-93)
+          q = pdf > 0.0f ? fminf(1.0f, norm(fv) / pdf) : 0.0f;
+          slot->gp = q;
+          if (!(rng_next(g) < q)) end = true;
+        }
         ro = hit_p;
         rd = normalize(to_world(fr, wi));
         rmin = BDPT_EPS_F;
         rmax = INFINITY;
         prev_f = fv;
         prev_n = n;
-        prev_pdf = pdf * 1.0f;
+        prev_pdf = pdf * q;
         prev_alpha = v.alpha;
         i++;
       }
@@ -1223,8 +1458,8 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       i = 2; count = 0; dm = 0;
     }
   }
-  eye_constants<MAXV>(S, P);
-  light_constants<MAXV>(S, P, lpp);
+  eye_constants<MAXV, EXT>(S, P);
+  light_constants<MAXV, EXT>(S, P, mis_p);
 }
 
 // What estimate_bidirection_radiance (bidirection.cpp:296-469) computes for pair (i, j) up to its
@@ -1240,26 +1475,35 @@ struct Conn {
 
 // A vertex that can receive a connection: diffuse (f != 0 only for DiffuseBSDF, bsdf.cpp:52-62),
 // viewed from its front side (wo.z >= 0) and carrying throughput.
-BDPT_HD bool can_connect(const Vtx& v) { return v.conn != 0; }
-template <class PA>
+BDPT_HD bool can_connect(const Vtx& v) { return v.cq > 0.0f; }
+template <bool EXT = false, class PA>
 BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   const bool eye_cam = i == 1;
   Vtx ev, lv;
   LightSample ls;
+  ls.env = false;
   EyeSample es;
   es.x = -1; es.y = -1;
   cn.splat = -1;
   if (!eye_cam) ev = P.e(i);
   if (j == 0) {
     if (eye_cam) return CONN_NONE;
+    if (EXT && is_env(ev)) {   // an escaped eye ray: the environment light contains it (§9)
+      const f3 c = env_radiance(S.env, neg(ev.n));
+      f3 contrib = mul(mul(ev.alpha, splat3(1.0f)), c);
+      float w = 0;
+      if (norm(contrib) > BDPT_EPS_F) w = mis_weight<EXT>(S, P, &ev, &lv, i, 0, ls, es, S.env.light, splat3(0), 0);
+      cn.val = muls(contrib, w);
+      return CONN_DIRECT;
+    }
     const DMat& M = S.mats[ev.mat];
     if (M.type != MAT_EMISSION) return CONN_NONE;
     f3 c = mk3(M.a[0], M.a[1], M.a[2]);
     if (!(norm(c) > BDPT_EPS_F)) return CONN_NONE;
     int eye_light = -1;
     for (int l = 0; l < S.nlights; l++)
-      if (light_contains(S.lights[l], ev.pos)) { eye_light = l; break; }
+      if ((!EXT || S.lights[l].type != LIGHT_ENV) && light_contains(S.lights[l], ev.pos)) { eye_light = l; break; }
     if (eye_light < 0) return CONN_NONE;
     f3 prevp = i == 2 ? cam : P.e(i - 1).pos;
     f3 wi = normalize(sub(ev.pos, prevp));
@@ -1268,7 +1512,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
     c = mk3(EL.rad[0], EL.rad[1], EL.rad[2]);
     f3 contrib = mul(mul(ev.alpha, splat3(1.0f)), c);
     float w = 0;
-    if (norm(contrib) > BDPT_EPS_F) w = mis_weight(S, P, &ev, &lv, i, 0, ls, es, eye_light, splat3(0), 0);
+    if (norm(contrib) > BDPT_EPS_F) w = mis_weight<EXT>(S, P, &ev, &lv, i, 0, ls, es, eye_light, splat3(0), 0);
     cn.val = muls(contrib, w);
     return CONN_DIRECT;
   }
@@ -1282,8 +1526,13 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
     rng_stream(g, 2u + (uint32_t)i);
     int id = (int)(rng_next(g) * (float)S.nlights);
     if (id >= S.nlights) id = S.nlights - 1;
-    float lp;
-    ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
+    if (EXT && S.lights[id].type == LIGHT_ENV) {
+      if (eye_cam) return CONN_NONE;   // no camera connection to a vertex at infinity (§9)
+      ls = env_sample_point(S, g, epos);
+    } else {
+      float lp;
+      ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);
+    }
     vl_pos = ls.pos; vl_n = ls.n; la = ls.alpha;
   } else {
     vl_pos = lv.pos; vl_n = lv.n; la = lv.alpha;
@@ -1299,9 +1548,17 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
   f3 eal = mul(ea, la);
   if (!nonzero3(eal)) return CONN_NONE;
   // One direction serves the f() hemisphere tests, the connection ray and both MIS endpoint steps.
-  f3 dc = sub(vl_pos, ve_pos);
-  float dist = norm(dc);
-  dc = normalize(dc);
+  const bool lenv = EXT && ls.env;
+  f3 dc;
+  float dist;
+  if (lenv) {
+    dc = neg(ls.n);   // toward the environment, unbounded
+    dist = INFINITY;
+  } else {
+    dc = sub(vl_pos, ve_pos);
+    dist = norm(dc);
+    dc = normalize(dc);
+  }
   f3 f_eye = splat3(1.0f), f_light = splat3(1.0f);
   if (!eye_cam) {
     if (lz(dc, ev.zh) < 0) return CONN_NONE;   // f_eye = 0 (bsdf.cpp:56-58)
@@ -1313,11 +1570,11 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
     const DMat& M = S.mats[lv.mat];
     f_light = divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
   }
-  float gg = fabsf(dot(vl_n, dc) * dot(ve_n, dc)) / (dist * dist);
+  float gg = lenv ? fabsf(dot(ve_n, dc)) : fabsf(dot(vl_n, dc) * dot(ve_n, dc)) / (dist * dist);
   f3 c = mul(muls(f_eye, gg), f_light);
   f3 contrib = mul(eal, c);
   if (!(norm(contrib) > BDPT_EPS_F)) return CONN_NONE;   // w = 0
-  float w = mis_weight(S, P, &ev, &lv, i, j, ls, es, -1, dc, dist);
+  float w = mis_weight<EXT>(S, P, &ev, &lv, i, j, ls, es, -1, dc, dist);
   f3 ill = muls(contrib, w);
   cn.o = ve_pos;
   cn.d = dc;
@@ -1333,16 +1590,16 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
 
 // One pixel-sample, connections resolved in the reference's (i, j) order (host/test use; the
 // device kernel defers the connection rays to a wave-compacted queue instead).
-template <int MAXV, int LM = 0, class Sink>
+template <int MAXV, int LM = 0, bool EXT = false, class Sink>
 BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt,
                          int x, int y, uint32_t sample, Sink& sink) {
   Rng g;
-  prepare_sample<MAXV, LM>(S, sp, P, cnt, g, x, y, sample);
+  prepare_sample<MAXV, LM, EXT>(S, sp, P, cnt, g, x, y, sample);
   f3 eye_sum = splat3(0);
   for (int i = 1; i < P.nE; i++) {
     for (int j = 0; j < P.nL; j++) {
       Conn cn;
-      int kind = make_conn(S, sp, PathsInRegs<MAXV>(P), g, i, j, cn);
+      int kind = make_conn<EXT>(S, sp, PathsInRegs<MAXV>(P), g, i, j, cn);
       if (kind == CONN_DIRECT) {
         eye_sum = add(eye_sum, cn.val);
       } else if (kind == CONN_RAY) {

@@ -21,6 +21,7 @@ enum { PIPE_WAVEFRONT = 0, PIPE_MEGAKERNEL = 1 };
 
 struct Ctx {
   HostScene hs;
+  bool ext = false;            // environment light or Russian roulette: the EXT kernels
   bdpt_params prm;
   int device = 0;
   int pipeline = PIPE_WAVEFRONT;
@@ -34,6 +35,7 @@ struct Ctx {
   DMat* d_mats = nullptr;
   DLight* d_lights = nullptr;
   int* d_prim_ref = nullptr;
+  float* d_env = nullptr;      // HostScene::env (environment light tables + map)
   float* d_eye = nullptr;
   float* d_light = nullptr;
   float* d_sample = nullptr;
@@ -72,6 +74,17 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.lgeom = nullptr;
   S.ntop = 0;
   S.cam = c->hs.cam;
+  const HostScene& hs = c->hs;
+  S.env.light = hs.env_light;
+  S.env.w = hs.env_w;
+  S.env.h = hs.env_h;
+  const size_t np = (size_t)hs.env_w * hs.env_h;
+  S.env.marg = c->d_env;
+  S.env.cond = c->d_env ? c->d_env + hs.env_h : nullptr;
+  S.env.pdf = c->d_env ? c->d_env + hs.env_h + np : nullptr;
+  S.env.rgb = c->d_env ? c->d_env + hs.env_h + 2 * np : nullptr;
+  S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];
+  S.env.rad = hs.env_rad;
   return S;
 }
 

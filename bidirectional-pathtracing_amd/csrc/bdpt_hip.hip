@@ -248,7 +248,9 @@ constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
 
 // LM (LDS mode): 0 = scene read from HBM/L2; 1 = whole BVH + geometry staged in LDS by every
 // block; 2 = the top n_top BFS-ordered nodes (the part every ray traverses) staged in LDS.
-template <int MAXV, bool STATS, int LM>
+// EXT: environment light and/or Russian roulette; EXT = false is the reference-only
+// path with no trace of either in the generated code.
+template <int MAXV, bool STATS, int LM, bool EXT>
 __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
   // One dynamic LDS array: [wave queues][optional scene / treelet copy]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       int nE = 0, nL = 0;
       PH_STAMP(tp0);
       if (t < my_n) {
-        prepare_sample<MAXV, LM>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
+        prepare_sample<MAXV, LM, EXT>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
         nE = P.nE;
         nL = P.nL;
         nsamp++;
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
         int kind = CONN_NONE;
         Conn cn;
         if (i < nE && j < nL) {
-          kind = make_conn(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn);
+          kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn);
           if (kind == CONN_DIRECT) {
             dxs += cn.val.x * inv;
             dys += cn.val.y * inv;
@@ -463,7 +465,7 @@ int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
   return BDPT_OK;
 }
 
-template <int MAXV, bool STATS>
+template <int MAXV, bool STATS, bool EXT>
 int launch_lm(Ctx* c, KParams& kp) {
   const size_t q = kWavesPerBlock * sizeof(WaveQ);
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
@@ -475,19 +477,20 @@ int launch_lm(Ctx* c, KParams& kp) {
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
-  if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1>, q + full, kp);
-  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
-  return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0>, q, kp);
+  if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, q + full, kp);
+  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
+  return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0, EXT>, q, kp);
 }
 
 template <int MAXV>
 int launch_maxv(Ctx* c, KParams& kp) {
-  return c->prm.collect_stats ? launch_lm<MAXV, true>(c, kp) : launch_lm<MAXV, false>(c, kp);
+  if (c->ext) return c->prm.collect_stats ? launch_lm<MAXV, true, true>(c, kp) : launch_lm<MAXV, false, true>(c, kp);
+  return c->prm.collect_stats ? launch_lm<MAXV, true, false>(c, kp) : launch_lm<MAXV, false, false>(c, kp);
 }
 
 void free_ctx(Ctx* c) {
   if (!c) return;
-  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref,
+  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env,
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -534,6 +537,12 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->pipeline = pipe == 2 ? PIPE_WAVEFRONT : PIPE_MEGAKERNEL;
   int rc = build_host_scene(scene, c->hs, g_err);
   if (rc) { delete c; return rc; }
+  c->ext = c->hs.env_light >= 0 || p.russian_roulette != 0;
+  if (c->ext && c->pipeline == PIPE_WAVEFRONT) {
+    g_err = "the wavefront pipeline does not implement the environment light / Russian roulette; use pipeline 0 or 1";
+    delete c;
+    return BDPT_E_UNSUPPORTED;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
     g_err = "no HIP device";
@@ -553,6 +562,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if ((rc = upload(&c->d_mats, c->hs.mats))) return fail(rc);
   if ((rc = upload(&c->d_lights, c->hs.lights))) return fail(rc);
   if ((rc = upload(&c->d_prim_ref, c->hs.prim_ref))) return fail(rc);
+  if (c->hs.env_light >= 0 && (rc = upload(&c->d_env, c->hs.env))) return fail(rc);
   c->npix = (size_t)p.width * p.height;
   size_t fb = c->npix * 3 * sizeof(float);
   if (hipMalloc((void**)&c->d_eye, fb) != hipSuccess || hipMalloc((void**)&c->d_light, fb) != hipSuccess ||
@@ -611,6 +621,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   KParams kp;
   kp.S = view_of(c, 0);   // launch_lm sets the LDS mode's view
   kp.sp.W = W; kp.sp.H = H; kp.sp.spp = c->prm.spp; kp.sp.max_depth = c->prm.max_depth; kp.sp.seed = c->prm.seed;
+  kp.sp.rr = c->prm.russian_roulette != 0;
   kp.eye = c->d_eye;
   kp.light = c->d_light;
   kp.stats = c->d_stats;

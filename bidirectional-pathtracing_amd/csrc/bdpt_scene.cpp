@@ -224,7 +224,7 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
     return BDPT_E_INVALID;
   }
   if (d->nmat <= 0 || !d->mats) { err = "scene has no materials"; return BDPT_E_INVALID; }
-  if (d->nlight <= 0 || !d->lights) { err = "scene has no light (BDPT needs one)"; return BDPT_E_INVALID; }
+  if ((d->nlight <= 0 || !d->lights) && !d->envmap) { err = "scene has no light (BDPT needs one)"; return BDPT_E_INVALID; }
   if (d->nprim >= (1 << 24)) { err = "too many primitives for the leaf encoding (2^24)"; return BDPT_E_INVALID; }
   // materials (collada.cpp:854-938 -> bsdf.h classes)
   out.mats.clear();
@@ -293,6 +293,67 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
       err = "unknown primitive type";
       return BDPT_E_INVALID;
     }
+  }
+  // environment light: appended after the scene's lights (raytraced_renderer.cpp:117-119)
+  out.env_light = -1;
+  out.env.clear();
+  if (d->envmap) {
+    const bdpt_envmap& em = *d->envmap;
+    if (em.width <= 0 || em.height <= 0 || !em.rgb || (long long)em.width * em.height > (1LL << 26)) {
+      err = "bad environment map";
+      return BDPT_E_INVALID;
+    }
+    const int w = em.width, h = em.height;
+    const size_t np = (size_t)w * h;
+    std::vector<double> pdf(np), marg(h), cond(np);
+    double sum = 0;
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        const float* t = em.rgb + 3 * ((size_t)w * j + i);
+        const double r = t[0], g = t[1], b = t[2];
+        const float il = (float)(0.2126f * r + 0.7152f * g + 0.0722f * b);   // Vector3D::illum() (float)
+        pdf[(size_t)w * j + i] = il * std::sin(PI_D * (j + .5) / h);
+        sum += pdf[(size_t)w * j + i];
+      }
+    if (!(sum > 0) || !std::isfinite(sum)) { err = "environment map has no positive radiance"; return BDPT_E_INVALID; }
+    for (int j = 0; j < h; ++j) {
+      const double prev = j == 0 ? 0 : marg[j - 1];
+      marg[j] = prev;
+      for (int i = 0; i < w; ++i) {
+        pdf[(size_t)w * j + i] /= sum;
+        marg[j] += pdf[(size_t)w * j + i];
+      }
+      const double py = marg[j] - prev;
+      for (int i = 0; i < w; i++) {   // a zero row is never selected; keep its CDF finite
+        const size_t k = (size_t)w * j + i;
+        cond[k] = (i == 0 ? 0 : cond[k - 1]) + (py > 0 ? pdf[k] / py : 1.0 / w);
+      }
+    }
+    out.env_w = w;
+    out.env_h = h;
+    out.env.resize((size_t)h + np * 2 + np * 3);
+    float* o = out.env.data();
+    for (int j = 0; j < h; j++) *o++ = (float)marg[j];
+    for (size_t k = 0; k < np; k++) *o++ = (float)cond[k];
+    for (size_t k = 0; k < np; k++) *o++ = (float)pdf[k];
+    for (size_t k = 0; k < np * 3; k++) *o++ = em.rgb[k];
+    // bounding sphere of the primitives (the emission disk's radius and centre)
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < 3; k++) { mn[k] = std::min(mn[k], pb[i].mn[k]); mx[k] = std::max(mx[k], pb[i].mx[k]); }
+    double ext2 = 0;
+    for (int k = 0; k < 3; k++) {
+      out.env_c[k] = (float)((mn[k] + mx[k]) / 2);
+      ext2 += (mx[k] - mn[k]) * (mx[k] - mn[k]);
+    }
+    const double R = std::sqrt(ext2) / 2;
+    out.env_rad = (float)R;
+    DLight L;
+    std::memset(&L, 0, sizeof L);
+    L.type = LIGHT_ENV;
+    L.area = (float)(PI_D * R * R);
+    out.env_light = (int)out.lights.size();
+    out.lights.push_back(L);
   }
   // the reference's tree: its DFS leaf order is the tie-break key of every primitive
   Builder R;

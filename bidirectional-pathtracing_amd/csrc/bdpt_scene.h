@@ -44,6 +44,12 @@ struct HostScene {
   int ref_nodes = 0;          // node count of the reference binary tree
   int dev_nodes = 0, dev_depth = 0;   // the device tree (SAH by default), binary
   int nprim = 0;
+  // environment light (bdpt_scene_desc.envmap): EnvironmentLight::init's tables
+  // (environment_light.cpp:18-62) built in fp64 and rounded, and the emission sphere
+  int env_light = -1;         // index in `lights`, -1 = none
+  int env_w = 0, env_h = 0;
+  std::vector<float> env;     // marginal_y[h] | conds_y[w*h] | pdf_envmap[w*h] | rgb[w*h*3]
+  float env_c[3] = {0, 0, 0}, env_rad = 0;
 };
 
 constexpr int kTopNodes = 1024;

@@ -203,7 +203,7 @@ struct PathsStore {
     r.alpha = mk3(c.x, c.y, c.z);
     const unsigned bits = __float_as_uint(c.w);
     r.mat = (int)(short)(bits & 0xffffu);
-    r.conn = (int)(bits >> 16);
+    r.cq = (bits >> 16) ? 1.0f : 0.0f;   // no roulette in this pipeline: q = 1
     return r;
   }
   __device__ Vtx e(int k) const { return ld(k - 2); }

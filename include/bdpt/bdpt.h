@@ -16,9 +16,16 @@
  * Plain C types only: no torch, no HIP types in any signature (a stream is passed as void*).
  * Every call returns 0 (BDPT_OK) or a negative BDPT_E_* code; bdpt_last_error() gives the text.
  * No C++ exception crosses this boundary. Unsupported features that the reference can only
- * assert(0) on under BDPT (microfacet sample_pdf, advanced_bsdf.cpp:144-148; environment /
- * directional / spot / sphere / mesh lights, light.cpp:25-51,168-194, environment_light.cpp:182-208)
- * are rejected at bdpt_create with BDPT_E_UNSUPPORTED instead of aborting.
+ * assert(0) on under BDPT (microfacet sample_pdf, advanced_bsdf.cpp:144-148; directional / spot /
+ * sphere / mesh lights, light.cpp:25-51,168-194) are rejected at bdpt_create with
+ * BDPT_E_UNSUPPORTED instead of aborting.
+ *
+ * Extensions beyond what the reference can run (semantics in DESIGN.md §9):
+ *   - the environment light under BDPT (the reference's EnvironmentLight has sample_L / sample_dir
+ *     but asserts in sample_Le / sample_Le_point / sample_pdf / contain_point,
+ *     environment_light.cpp:182-208): bdpt_scene_desc.envmap, loaded by bdpt_exr_load (-e);
+ *   - Russian roulette on both subpaths through PathVertex.q (bidirection.h:36, the rule commented
+ *     out at bidirection.cpp:87-93): bdpt_params.russian_roulette.
  */
 #ifndef BDPT_AMD_BDPT_H
 #define BDPT_AMD_BDPT_H
@@ -30,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 1
+#define BDPT_ABI_VERSION 2
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -53,7 +60,8 @@ enum bdpt_mat_type {
   BDPT_MAT_MICROFACET = 5   /* rejected: sample_pdf asserts under BDPT  advanced_bsdf.cpp:144-148 */
 };
 
-/* Light kinds (src/scene/light.h). Only area and point lights have BDPT methods. */
+/* Light kinds (src/scene/light.h). Only area and point lights have BDPT methods in the reference;
+ * the environment light comes in through bdpt_scene_desc.envmap, never through this list. */
 enum bdpt_light_type { BDPT_LIGHT_AREA = 0, BDPT_LIGHT_POINT = 1, BDPT_LIGHT_OTHER = 2 };
 
 typedef struct bdpt_material {
@@ -85,6 +93,13 @@ typedef struct bdpt_camera {
   double fclip;
 } bdpt_camera;
 
+/* The HDRImageBuffer of an environment map (main.cpp:40-77 load_exr; data[w*j + i], row j = 0 at
+ * theta = 0, i.e. +y): EnvironmentLight(envMap) (environment_light.cpp:6-62). */
+typedef struct bdpt_envmap {
+  int32_t width, height;
+  const float* rgb;           /* width*height*3                                          */
+} bdpt_envmap;
+
 /* Scene in the reference's primitive order (objects in scene order, faces in mesh order:
  * RaytracedRenderer::build_accel, raytraced_renderer.cpp:350-374). The BVH is built from it. */
 typedef struct bdpt_scene_desc {
@@ -97,6 +112,9 @@ typedef struct bdpt_scene_desc {
   int32_t nlight;
   const bdpt_light* lights;
   bdpt_camera camera;
+  /* NULL = none. Otherwise an EnvironmentLight appended after `lights` (the renderer pushes
+   * pt->envLight onto scene->lights last, raytraced_renderer.cpp:117-119). ABI v2. */
+  const bdpt_envmap* envmap;
 } bdpt_scene_desc;
 
 /* Random-number semantics of the device path: Philox4x32-10 keyed by seed, counter
@@ -111,7 +129,8 @@ typedef struct bdpt_params {
   int32_t device;             /* HIP device ordinal                                       */
   int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
   int32_t pipeline;           /* 0 = auto, 1 = megakernel, 2 = wavefront; same results     */
-  int32_t reserved[4];
+  int32_t russian_roulette;   /* 1 = PathVertex.q roulette on both subpaths (ABI v2)       */
+  int32_t reserved[3];
 } bdpt_params;
 
 typedef struct bdpt_tile {
@@ -187,6 +206,14 @@ int bdpt_dae_get_desc(const bdpt_dae* scene, bdpt_scene_desc* out);
 /* Writes the scene in the JSON dump format of tests/golden/scenes (round-trip doubles). */
 int bdpt_dae_dump_json(const bdpt_dae* scene, const char* path);
 void bdpt_dae_free(bdpt_dae* scene);
+
+/* Host-side OpenEXR reader for the -e environment map (main.cpp:40-77 load_exr, tinyexr):
+ * scanline files with NONE / RLE / ZIPS / ZIP compression and HALF / FLOAT / UINT channels.
+ * Like load_exr, the channels are taken in the file's (alphabetical) channel-list order and
+ * r, g, b = channels 2, 1, 0 (an RGB file: R, G, B). *rgb_out (width*height*3 floats) is freed
+ * with bdpt_exr_free. */
+int bdpt_exr_load(const char* path, int32_t* width, int32_t* height, float** rgb_out);
+void bdpt_exr_free(float* rgb);
 
 #ifdef __cplusplus
 }

@@ -171,6 +171,7 @@ struct PolicyRef {              // mode 0
   static R pow4(R x) { return std::pow(x, 4); }
   static R pow5(R x) { return std::pow(x, 5); }
   static R tan_half_fov(double fov_deg) { return std::tan(fov_deg * PI_D / 360); }
+  static const bool kDevEnv = false;   // environment map math: the reference's libm formulas
 };
 struct PolicyC64 {              // mode 1
   typedef double R;
@@ -186,6 +187,7 @@ struct PolicyC64 {              // mode 1
   static R pow4(R x) { return std::pow(x, 4); }
   static R pow5(R x) { return std::pow(x, 5); }
   static R tan_half_fov(double fov_deg) { return std::tan(fov_deg * PI_D / 360); }
+  static const bool kDevEnv = false;
 };
 
 // Deterministic fp32 sin/cos of 2*pi*u, u in (0,1): quadrant reduction (exact by Sterbenz) and
@@ -211,6 +213,31 @@ static inline void cos_sin_2pi_f32(float u, float* c, float* s) {
   }
 }
 
+// Deterministic fp32 atan2 (octant reduction + the Cephes atanf polynomial), the device's
+// atan2_det in the same operation order: the environment map's direction -> (theta, phi) in mode 2.
+static inline float atan2_f32(float y, float x) {
+  const float ax = std::fabs(x), ay = std::fabs(y);
+  if (ax == 0.0f && ay == 0.0f) return 0.0f;
+  float t = ay <= ax ? ay / ax : ax / ay;
+  float off = 0.0f;
+  if (t > 0.41421356237309503f) {
+    off = 0.78539816339744831f;
+    t = (t - 1.0f) / (t + 1.0f);
+  }
+  const float z = t * t;
+  float r = ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z) * t + t;
+  r = off + r;
+  if (ay > ax) r = 1.57079632679489662f - r;
+  if (x < 0.0f) r = 3.14159265358979323f - r;
+  return y < 0.0f ? -r : r;
+}
+// std::lround for x >= 0 (halves away from zero)
+template <class R>
+static inline long lround_pos(R x) {
+  const R f = std::floor(x);
+  return (long)f + ((x - f) >= R(0.5) ? 1 : 0);
+}
+
 struct PolicyC32 {              // mode 2
   typedef float R;
   // The device sums the power-heuristic terms in Horner form over per-vertex prefixes
@@ -227,6 +254,7 @@ struct PolicyC32 {              // mode 2
   static R pow4(R x) { R x2 = x * x; return x2 * x2; }
   static R pow5(R x) { R x2 = x * x; R x4 = x2 * x2; return x4 * x; }
   static R tan_half_fov(double fov_deg) { return (float)std::tan(fov_deg * PI_D / 360); }
+  static const bool kDevEnv = true;    // environment map math: the device's deterministic forms
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -277,6 +305,18 @@ struct Light {
   R area;
 };
 
+// The environment light (EnvironmentLight, environment_light.cpp): its map, the
+// sampling tables of init() (:18-62) in fp64 rounded to R, and the emission sphere.
+static const int LIGHT_ENV_ORC = 100;   // Light::type of the environment light (internal)
+template <class R>
+struct EnvMap {
+  int w = 0, h = 0;
+  std::vector<R> marg, cond, pdf;
+  std::vector<V3<R>> rgb;
+  V3<R> center;
+  R rad = 0, area = 0;   // area = pi R^2 (the emission disk)
+};
+
 struct BvhNode {
   int l = -1, r = -1;      // children (-1: leaf)
   int start = 0, end = 0;  // leaf range into leaf_prims
@@ -298,6 +338,8 @@ struct Scene {
   V3<R> c2w[3], w2c[3];  // columns
   double hfov_deg, vfov_deg;
   R nclip, fclip;
+  EnvMap<R> env;
+  int env_light = -1;              // index in lights, -1: none
 };
 
 // BVH build: construct_bvh (bvh.cpp:51-129) in fp64 on the reference's bboxes.
@@ -424,7 +466,7 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) 
     M.ior = (R)m.ior;
     sc.mats.push_back(M);
   }
-  if (d->nlight < 1) { err = "scene has no light"; return BDPT_E_INVALID; }
+  if (d->nlight < 1 && !d->envmap) { err = "scene has no light"; return BDPT_E_INVALID; }
   for (int i = 0; i < d->nlight; i++) {
     const bdpt_light& l = d->lights[i];
     if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT) {
@@ -466,6 +508,63 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) 
       }
     }
   }
+  // Environment light, appended after the scene's lights (raytraced_renderer.cpp:117-119); tables
+  // as EnvironmentLight::init (environment_light.cpp:18-62) in fp64.
+  if (d->envmap) {
+    const bdpt_envmap& em = *d->envmap;
+    if (em.width <= 0 || em.height <= 0 || !em.rgb) { err = "bad environment map"; return BDPT_E_INVALID; }
+    const int w = em.width, h = em.height;
+    const size_t np = (size_t)w * h;
+    std::vector<double> pdf(np), marg(h), cond(np);
+    double sum = 0;
+    for (int j = 0; j < h; ++j) {
+      for (int i = 0; i < w; ++i) {
+        const float* t = em.rgb + 3 * ((size_t)w * j + i);
+        V3<double> px(t[0], t[1], t[2]);                                      // main.cpp:70-74
+        float illum = 0.2126f * px.x + 0.7152f * px.y + 0.0722f * px.z;        // vector3D.h:231-233
+        pdf[(size_t)w * j + i] = illum * std::sin(PI_D * (j + .5) / h);
+        sum += pdf[(size_t)w * j + i];
+      }
+    }
+    if (!(sum > 0)) { err = "environment map has no positive radiance"; return BDPT_E_INVALID; }
+    for (int j = 0; j < h; ++j) {
+      double prev = j == 0 ? 0 : marg[j - 1];
+      marg[j] = prev;
+      for (int i = 0; i < w; ++i) {
+        pdf[(size_t)w * j + i] /= sum;
+        marg[j] += pdf[(size_t)w * j + i];
+      }
+      double py = marg[j] - prev;
+      for (int i = 0; i < w; i++) {   // (a zero row, never selected, gets a finite CDF)
+        size_t k = (size_t)w * j + i;
+        cond[k] = i == 0 ? 0 : cond[k - 1];
+        cond[k] += py > 0 ? pdf[k] / py : 1.0 / w;
+      }
+    }
+    EnvMap<R>& E = sc.env;
+    E.w = w;
+    E.h = h;
+    E.marg.assign(marg.begin(), marg.end());
+    E.cond.assign(cond.begin(), cond.end());
+    E.pdf.assign(pdf.begin(), pdf.end());
+    E.rgb.resize(np);
+    for (size_t k = 0; k < np; k++) E.rgb[k] = V3<R>((R)em.rgb[3 * k], (R)em.rgb[3 * k + 1], (R)em.rgb[3 * k + 2]);
+    // bounding sphere of all primitives: centre of the box, radius half its diagonal
+    BBoxT<double> all_box = pb[0];
+    for (int i = 1; i < d->nprim; i++) all_box.expand(pb[i]);
+    V3<double> ctr((all_box.mn.x + all_box.mx.x) / 2, (all_box.mn.y + all_box.mx.y) / 2,
+                   (all_box.mn.z + all_box.mx.z) / 2);
+    V3<double> ext = all_box.mx - all_box.mn;
+    double rad = std::sqrt(ext.x * ext.x + ext.y * ext.y + ext.z * ext.z) / 2;
+    E.center = cvt<R>(ctr);
+    E.rad = (R)rad;
+    E.area = (R)(PI_D * rad * rad);
+    Light<R> L;
+    L.type = LIGHT_ENV_ORC;
+    L.area = E.area;
+    sc.env_light = (int)sc.lights.size();
+    sc.lights.push_back(L);
+  }
   // Camera
   const bdpt_camera& c = d->camera;
   sc.cam_pos = cvt<R>(v3d(c.pos));
@@ -478,6 +577,96 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) 
   sc.nclip = (R)c.nclip;
   sc.fclip = (R)c.fclip;
   return BDPT_OK;
+}
+
+// ----------------------------------------------------------------------------------------------
+// EnvironmentLight math (environment_light.cpp). Modes 0/1 (P::kDevEnv false) follow the
+// reference's libm expressions exactly (pinned by tests/test_env.py against the reference's own
+// EnvironmentLight); mode 2 the device's deterministic forms (bdpt_core.h env_*).
+template <class R>
+static int upper_idx(const std::vector<R>& a, size_t off, int n, R u) {   // std::upper_bound, <= n-1
+  int k = (int)(std::upper_bound(a.begin() + off, a.begin() + off + n, u) - (a.begin() + off));
+  return k < n ? k : n - 1;
+}
+template <class R>
+static V3<R> env_bilerp(const EnvMap<R>& E, R x, R y) {                      // :106-123
+  long right = lround_pos(x), left, v = lround_pos(y);
+  R u1 = right - x + R(.5), v1;
+  if (right == 0 || right == E.w) {
+    left = E.w - 1;
+    right = 0;
+  } else left = right - 1;
+  if (v == 0) v1 = v = 1;
+  else if (v == E.h) {
+    v = E.h - 1;
+    v1 = 0;
+  } else v1 = v - y + R(.5);
+  long bottom = E.w * v, top = bottom - E.w;
+  R u0 = 1 - u1;
+  return (E.rgb[top + left] * u1 + E.rgb[top + right] * u0) * v1 +
+         (E.rgb[bottom + left] * u1 + E.rgb[bottom + right] * u0) * (1 - v1);
+}
+// xy_to_theta_phi + theta_phi_to_dir (:88-104)
+template <class P, class R>
+static V3<R> env_xy_to_dir(const EnvMap<R>& E, R x, R y, R* sin_theta) {
+  if (P::kDevEnv) {
+    R cp, sp, ct, st;
+    P::cos_sin_2pi(x / R(E.w), &cp, &sp);
+    P::cos_sin_2pi((y / R(E.h)) * R(0.5), &ct, &st);
+    *sin_theta = st;
+    return V3<R>(-cp * st, ct, sp * st);
+  }
+  double phi = x / E.w * 2.0 * PI_D;
+  double theta = y / E.h * PI_D;
+  *sin_theta = (R)std::sin(theta);
+  return V3<R>((R)(std::cos(phi - PI_D) * std::sin(theta)), (R)std::cos(theta),
+               (R)(-std::sin(phi - PI_D) * std::sin(theta)));
+}
+// dir_to_theta_phi + theta_phi_to_xy (:81-86, 97-102). Mode 2 takes the direction as unit.
+template <class P, class R>
+static void env_dir_to_xy(const EnvMap<R>& E, const V3<R>& d, R* x, R* y, R* sin_theta) {
+  if (P::kDevEnv) {
+    const R st = std::sqrt(std::max(R(0), (R(1) - d.y) * (R(1) + d.y)));
+    const R th = atan2_f32(st, d.y);
+    const R ph = atan2_f32(-d.z, d.x) + R(PI_D);
+    *x = ph / R(2) / R(PI_D) * R(E.w);
+    *y = th / R(PI_D) * R(E.h);
+    *sin_theta = st;
+    return;
+  }
+  V3<R> u = d.unit();
+  double theta = std::acos(u.y);
+  double phi = std::atan2(-u.z, u.x) + PI_D;
+  *x = (R)(phi / 2. / PI_D * E.w);
+  *y = (R)(theta / PI_D * E.h);
+  *sin_theta = (R)std::sin(theta);
+}
+template <class P, class R>
+static V3<R> env_radiance(const EnvMap<R>& E, const V3<R>& d) {             // sample_dir (:159-168)
+  R x, y, st;
+  env_dir_to_xy<P>(E, d, &x, &y, &st);
+  return env_bilerp(E, x, y);
+}
+// solid-angle pdf of sample_L choosing direction d; 0 at the poles
+template <class P, class R>
+static R env_pdf_dir(const EnvMap<R>& E, const V3<R>& d) {
+  R x, y, st;
+  env_dir_to_xy<P>(E, d, &x, &y, &st);
+  if (!(st > 0)) return 0;
+  int i = std::min((int)x, E.w - 1), j = std::min((int)y, E.h - 1);
+  return E.pdf[(size_t)E.w * j + i] * R(E.w * E.h) / (R(2) * R(PI_D) * R(PI_D) * st);
+}
+// sample_L's direction sampling (:126-156) from explicit uniforms: (ux, uy) the grid sample,
+// (jx, jy) the texel jitter.
+template <class P, class R>
+static V3<R> env_sample_dir(const EnvMap<R>& E, R ux, R uy, R jx, R jy, V3<R>* wi, R* pdf) {
+  int y = upper_idx(E.marg, 0, E.h, uy);
+  int x = upper_idx(E.cond, (size_t)E.w * y, E.w, ux);
+  R xf = x + jx, yf = y + jy;
+  R st;
+  *wi = env_xy_to_dir<P>(E, xf, yf, &st);
+  *pdf = E.pdf[(size_t)E.w * y + x] * R(E.w * E.h) / (R(2) * R(PI_D) * R(PI_D) * st);
+  return env_bilerp(E, xf, yf);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -494,6 +683,10 @@ struct Tracer {
   int max_depth, W, H, ns_aa;
   R tanh_, tanv_;
   Stats st;
+  bool rr = false;   // Russian roulette: PathVertex.q, bidirection.cpp:87-93
+  // L[1]'s MIS densities when the light subpath starts on the environment light
+  bool l1_env = false;
+  R l1_mis_p = 0, l1_mis_dir = 0;
   // splat sink (lightBuffer & sampleBuffer updates, bidirection.cpp:457-466)
   std::vector<double>* light_buf = nullptr;   // W*H*3
   std::vector<double>* sample_buf = nullptr;  // mode 0 only (exact sampleBuffer order)
@@ -510,6 +703,7 @@ struct Tracer {
     V alpha = V(1), position;
     bool is_light = false, new_sample = false;
     R dir_pdf = 0;
+    bool env = false;       // environment vertex at infinity: isect.n = -w
   };
 
   Tracer(const Scene<R>& s, P p, int md, int w, int h, int spp)
@@ -743,6 +937,31 @@ struct Tracer {
 
   // ---------------- lights (light.cpp) ----------------
   V light_sample_Le(const Light<R>& L, Ray<R>* ray, R* point_pdf, R* dir_pdf, V* normal) {
+    l1_env = false;
+    if (L.type == LIGHT_ENV_ORC) {   // importance-sampled w, origin on the disk facing -w
+      const EnvMap<R>& E = sc.env;
+      R ux, uy;
+      grid2d(&ux, &uy);
+      R jx = pol.uS();
+      R jy = pol.uS();
+      V w;
+      R pw;
+      V Le = env_sample_dir<P>(E, ux, uy, jx, jy, &w, &pw);
+      R u1 = pol.uS(), u2 = pol.uS();
+      R r = E.rad * std::sqrt(u1);
+      R c, s;
+      P::cos_sin_2pi(u2, &c, &s);
+      Frame<R> f = make_coord_space(w);
+      ray->o = E.center + E.rad * w + (r * c) * f.X + (r * s) * f.Y;
+      ray->d = -w; ray->min_t = 0; ray->max_t = (R)INFINITY;
+      *point_pdf = R(1) / E.area;
+      *dir_pdf = pw;
+      *normal = -w;
+      l1_env = true;
+      l1_mis_p = pw;
+      l1_mis_dir = R(1) / E.area;
+      return Le;
+    }
     if (L.type == BDPT_LIGHT_POINT) {                                        // :115-123
       V d = sphere_uniform();
       ray->o = L.position; ray->d = d; ray->min_t = 0; ray->max_t = (R)INFINITY;
@@ -765,6 +984,20 @@ struct Tracer {
   }
   V light_sample_Le_point(const Light<R>& L, const V& p, V* wi, V* point, R* dist, R* point_pdf,
                           R* dir_pdf, V* normal) {
+    if (L.type == LIGHT_ENV_ORC) {   // a vertex at infinity in direction w
+      R ux, uy;
+      grid2d(&ux, &uy);
+      R jx = pol.uS();
+      R jy = pol.uS();
+      R pw;
+      V Le = env_sample_dir<P>(sc.env, ux, uy, jx, jy, wi, &pw);
+      *point = p;
+      *dist = (R)INFINITY;
+      *point_pdf = pw;
+      *dir_pdf = R(1) / sc.env.area;
+      *normal = -(*wi);
+      return Le;
+    }
     if (L.type == BDPT_LIGHT_POINT) {                                        // :125-137
       V d = L.position - p;
       *wi = d.unit();
@@ -797,6 +1030,14 @@ struct Tracer {
     V d = L.position - p;                                                     // :257-262
     d.normalize();
     return std::fabs(dot(d, L.direction)) < R(EPS_F);
+  }
+  // env light: only ever asked about an environment vertex (direction -n) or, for
+  // the step below one, about the planar density of its emission disk
+  V env_light_pdf(const Vertex& v, R* point_pdf, R* dir_pdf) const {
+    const V w = -v.isect.n;
+    *point_pdf = env_pdf_dir<P>(sc.env, w) / R(sc.lights.size());
+    *dir_pdf = R(1) / sc.env.area;
+    return env_radiance<P>(sc.env, w);
   }
   V light_sample_pdf(const Light<R>& L, const V& p, const V& wi, R* point_pdf, R* dir_pdf) const {
     if (!light_contain_point(L, p)) { *point_pdf = 0.; *dir_pdf = 0.; return V(); }
@@ -864,11 +1105,29 @@ struct Tracer {
     v.is_light = is_light;
     v.dir_pdf = dir_pdf;
     path.push_back(v);
+    if (is_light && l1_env) {   // env light: L[1]'s MIS densities
+      path[1].env = true;
+      path[1].p = l1_mis_p / R(sc.lights.size());
+      path[1].dir_pdf = l1_mis_dir;
+    }
+    v.env = false;
     int i = 2;
     Isect isect;
     R prev_pdf = dir_pdf;
     V prev_f(1., 1., 1.), prev_n(init_normal);
-    while (intersect(r, &isect, true)) {
+    for (;;) {
+      if (!intersect(r, &isect, true)) {
+        if (!is_light && sc.env_light >= 0) {   // the escaped eye ray ends on the environment
+          Vertex e;
+          e.env = true;
+          e.isect.n = -r.d;
+          e.position = r.o;
+          e.alpha = path[i - 1].alpha * std::fabs(dot(prev_n, r.d)) * prev_f / prev_pdf;
+          e.q = 1.;
+          path.push_back(e);
+        }
+        break;
+      }
       r.max_t = isect.t;  // (not read again: the next ray is rebuilt below)
       Frame<R> f = make_coord_space(isect.n);
       const V hit_p = r.o + r.d * isect.t;
@@ -891,6 +1150,11 @@ struct Tracer {
       v.q = p_keep;
       path.push_back(v);
       if (i >= max_depth + 1) break;
+      if (rr && i > 3) {   // bidirection.cpp:87-93 with min_subpath_length = 3 (BDPT_RR_MIN)
+        p_keep = pdf > 0 ? std::min(R(1), fv.norm() / pdf) : R(0);
+        path.back().q = p_keep;
+        if (!(pol.uS() < p_keep)) break;   // coin_flip(p_keep)
+      }
       prev_f = fv;
       prev_n = isect.n;
       prev_pdf = pdf * p_keep;
@@ -915,106 +1179,118 @@ struct Tracer {
     return s == R(0.) ? R(0.) : (f * f) * s;
   }
 
+  // One MIS step (bidirection.cpp:151-158 and the five copies that follow): d = unit(cur - oth),
+  // g = |(frame(oth.n)^T d).z * dot(d, cur.n)| / dist^2, with the environment rules of DESIGN.md §9
+  // (oth env: d = oth.n = -w, g = |dot(d, cur.n)|; cur env: d = -cur.n = w, g = 1).
+  R step(const Vertex& cur, const Vertex& oth, V* d_out) const {
+    if (cur.env) { *d_out = -cur.isect.n; return R(1.); }
+    if (oth.env) { *d_out = oth.isect.n; return std::fabs(dot(oth.isect.n, cur.isect.n)); }
+    Frame<R> f = make_coord_space(oth.isect.n);
+    V wi_world = cur.position - oth.position;
+    R dist = wi_world.norm();
+    wi_world.normalize();
+    V wi = f.to_local(wi_world);
+    *d_out = wi_world;
+    return std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+  }
+  R pdf_from(const Vertex& v, const V& d) const {   // v.bsdf->sample_pdf(0, frame(v.n)^T d)
+    V wo;
+    return bsdf_sample_pdf(v.isect.mat, wo, make_coord_space(v.isect.n).to_local(d));
+  }
+
   R mis_weight(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L,
                const Vertex& LS, const Vertex& ES) {                          // :121-293
     R w_inv = 0., ratio = 1.;
     w_inv += ratio;
     R fE[64], fL[64];
     bool tE[64], tL[64];
-    const Light<R>* eye_light = nullptr;
+    int eye_light = -1;
     for (int i = i_eye; i > 1; i--) {
       const Vertex& cur = E[i];
       const Vertex& prv = (i == i_eye) ? (i_light == 1 ? LS : L[i_light]) : E[i + 1];
       const Vertex& nxt = E[i - 1];
       R nom, denom, p = 0, g;
-      Frame<R> f = make_coord_space(prv.isect.n);
-      V wo, wi_world = cur.position - prv.position;
-      R dist = wi_world.norm();
-      wi_world.normalize();
-      V wi = f.to_local(wi_world);
-      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      V d;
       if (i_light == 0 && i == i_eye) {
-        bool hit = false;
-        for (size_t j = 0; j < sc.lights.size(); j++) {
-          if (light_contain_point(sc.lights[j], cur.position)) {
-            hit = true;
-            eye_light = &sc.lights[j];
-            g = 1.;
-            R pp, dp;
-            light_sample_pdf(sc.lights[j], cur.position, V(), &pp, &dp);
-            p = pp;
-            break;
-          }
+        // the light containing cur: the env light for an environment vertex, else the first
+        // area / point light whose contain_point holds (the env light contains no surface point)
+        if (cur.env) {
+          eye_light = sc.env_light;
+        } else {
+          for (size_t j = 0; j < sc.lights.size(); j++)
+            if (sc.lights[j].type != LIGHT_ENV_ORC && light_contain_point(sc.lights[j], cur.position)) {
+              eye_light = (int)j;
+              break;
+            }
         }
-        if (!hit) return 0.;
-      } else if (i_light == 1 && i == i_eye) {
-        p = LS.dir_pdf * LS.q;
-      } else if (i_light == 0 && i == i_eye - 1) {
+        if (eye_light < 0) return 0.;
+        g = 1.;
         R pp, dp;
-        V w = -wi_world;
-        light_sample_pdf(*eye_light, prv.position, w, &pp, &dp);
-        p = dp * L[1].q;
+        if (cur.env) env_light_pdf(cur, &pp, &dp);
+        else light_sample_pdf(sc.lights[eye_light], cur.position, V(), &pp, &dp);
+        p = pp;
       } else {
-        p = bsdf_sample_pdf(prv.isect.mat, wo, wi) * prv.q;
+        g = step(cur, prv, &d);
+        if (i_light == 1 && i == i_eye) {
+          p = LS.dir_pdf * LS.q;
+        } else if (i_light == 0 && i == i_eye - 1) {
+          R pp, dp;
+          if (prv.env) env_light_pdf(prv, &pp, &dp);
+          else light_sample_pdf(sc.lights[eye_light], prv.position, -d, &pp, &dp);
+          p = dp * L[1].q;
+        } else {
+          p = pdf_from(prv, d) * prv.q;
+        }
       }
       nom = p * g;
-      f = make_coord_space(nxt.isect.n);
-      wi_world = cur.position - nxt.position;
-      dist = wi_world.norm();
-      wi_world.normalize();
-      wi = f.to_local(wi_world);
-      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      g = step(cur, nxt, &d);
       if (i == 2) {
         p = 1.;
         g = 1.;
       } else {
-        p = bsdf_sample_pdf(nxt.isect.mat, wo, wi) * nxt.q;
+        p = pdf_from(nxt, d) * nxt.q;
       }
       denom = p * g;
+      // an environment vertex right after the camera has no camera-connection strategy (§9)
+      const bool t = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) && !(cur.env && i == 2);
       if (P::kHornerMis) {
         fE[i] = nom / denom;
-        tE[i] = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat));
+        tE[i] = t;
         continue;
       }
       ratio *= nom / denom;
-      if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
+      if (!t) continue;
       w_inv += ratio * ratio;
     }
     ratio = 1.;
     for (int i = i_light; i > 0; i--) {
-      const Vertex& cur = L[i];
+      // environment scenes: the light end of (i, 1) is the fresh sample itself;
+      // otherwise the reference's original L[1] (quirk 5)
+      const Vertex& cur = (i == 1 && i_light == 1 && sc.env_light >= 0) ? LS : L[i];
       const Vertex& prv = (i == i_light) ? (i_eye == 1 ? ES : E[i_eye]) : L[i + 1];
       const Vertex& nxt = L[i - 1];
       R nom, denom, p, g;
-      Frame<R> f = make_coord_space(prv.isect.n);
-      V wo, wi_world = cur.position - prv.position;
-      R dist = wi_world.norm();
-      wi_world.normalize();
-      V wi = f.to_local(wi_world);
+      V d;
+      g = step(cur, prv, &d);
       if (i_eye <= 1 && i == i_light) p = ES.dir_pdf * ES.q;
-      else p = bsdf_sample_pdf(prv.isect.mat, wo, wi) * prv.q;
-      g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+      else p = pdf_from(prv, d) * prv.q;
       nom = p * g;
       if (i > 1) {
-        f = make_coord_space(nxt.isect.n);
-        wi_world = cur.position - nxt.position;
-        dist = wi_world.norm();
-        wi_world.normalize();
-        wi = f.to_local(wi_world);
+        g = step(cur, nxt, &d);
         if (i == 2) p = nxt.dir_pdf;
-        else p = bsdf_sample_pdf(nxt.isect.mat, wo, wi) * nxt.q;
-        g = std::fabs(wi.z * dot(wi_world, cur.isect.n)) / (dist * dist);
+        else p = pdf_from(nxt, d) * nxt.q;
         denom = p * g;
       } else {
         denom = cur.p;
       }
+      const bool t = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat));
       if (P::kHornerMis) {
         fL[i] = nom / denom;
-        tL[i] = !(is_delta(cur.isect.mat) || is_delta(nxt.isect.mat));
+        tL[i] = t;
         continue;
       }
       ratio *= nom / denom;
-      if (is_delta(cur.isect.mat) || is_delta(nxt.isect.mat)) continue;
+      if (!t) continue;
       w_inv += ratio * ratio;
     }
     if (P::kHornerMis) {
@@ -1037,16 +1313,20 @@ struct Tracer {
   V estimate(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L) {  // :296-469
     Vertex ve, vl, LS, ES;
     int eye_x = -1, eye_y = -1;
+    if (i_eye > 1 && E[i_eye].env && i_light >= 1) return V();   // nothing connects to infinity
     ve = E[i_eye];
     vl = L[i_light];
     V c;
     if (i_light == 0) {
-      if (i_eye > 1) {
+      if (i_eye > 1 && E[i_eye].env) {   // an escaped eye ray: the environment's radiance (§9)
+        R pp, dp;
+        c = env_light_pdf(E[i_eye], &pp, &dp);
+      } else if (i_eye > 1) {
         c = get_emission(E[i_eye].isect.mat);
         if (c.norm() > R(EPS_F)) {
           bool hit = false;
           for (size_t j = 0; j < sc.lights.size(); j++) {
-            if (light_contain_point(sc.lights[j], E[i_eye].position)) {
+            if (sc.lights[j].type != LIGHT_ENV_ORC && light_contain_point(sc.lights[j], E[i_eye].position)) {
               hit = true;
               R pp, dp;
               V wi = E[i_eye].position - E[i_eye - 1].position;
@@ -1077,8 +1357,10 @@ struct Tracer {
         LS.is_light = true;
         LS.new_sample = true;
         LS.dir_pdf = ldp;
+        LS.env = sc.lights[id].type == LIGHT_ENV_ORC;
         f_light = V(1., 1., 1.);
         vl = LS;
+        if (LS.env && i_eye == 1) return V();   // no camera connection to infinity (§9)
       }
       if (i_eye == 1) {
         V edir, epoint, en;
@@ -1100,8 +1382,12 @@ struct Tracer {
         V er = E[i_eye - 1].position - E[i_eye].position;
         er.normalize();
         er = f.to_local(er);
-        connect = vl.position - E[i_eye].position;
-        connect.normalize();
+        if (vl.env) {
+          connect = -vl.isect.n;
+        } else {
+          connect = vl.position - E[i_eye].position;
+          connect.normalize();
+        }
         connect = f.to_local(connect);
         f_eye = bsdf_f(E[i_eye].isect.mat, er, connect);
       }
@@ -1115,9 +1401,15 @@ struct Tracer {
         connect = f.to_local(connect);
         f_light = bsdf_f(L[i_light].isect.mat, connect, lr);
       }
-      connect = vl.position - ve.position;
-      R dist = connect.norm();
-      connect.normalize();
+      R dist;
+      if (vl.env) {   // toward the environment, unbounded; G = |cos| at the eye end only (§9)
+        connect = -vl.isect.n;
+        dist = (R)INFINITY;
+      } else {
+        connect = vl.position - ve.position;
+        dist = connect.norm();
+        connect.normalize();
+      }
       Ray<R> r;
       r.o = ve.position;
       r.d = connect;
@@ -1125,7 +1417,8 @@ struct Tracer {
       r.max_t = dist - R(EPS_F);
       Isect is;
       if (intersect(r, &is, false)) return V();
-      R g = std::fabs(dot(vl.isect.n, connect) * dot(ve.isect.n, connect)) / (dist * dist);
+      R g = vl.env ? std::fabs(dot(ve.isect.n, connect))
+                   : std::fabs(dot(vl.isect.n, connect) * dot(ve.isect.n, connect)) / (dist * dist);
       c = f_eye * g * f_light;
     }
     V la = i_light == 1 ? LS.alpha : L[i_light].alpha;
@@ -1197,7 +1490,8 @@ struct Tracer {
 // ----------------------------------------------------------------------------------------------
 template <class R>
 static int render_counter(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, uint64_t seed,
-                          int s0, int sc_count, int nthreads, double* eye, double* light, double* stats) {
+                          int s0, int sc_count, int nthreads, double* eye, double* light, double* stats,
+                          int rr) {
   Scene<R> sc;
   std::string err;
   int rc = load_scene<R>(d, sc, err);
@@ -1216,6 +1510,7 @@ static int render_counter(const bdpt_scene_desc* d, int W, int H, int spp, int m
           P pol;
           pol.cs = &cs;
           Tracer<P> tr(sc, pol, max_depth, W, H, spp);
+          tr.rr = rr != 0;
           tr.light_buf = &lbuf[t];
           V3<R> ill = tr.one_sample(x, y);
           R inv = R(1.) / R(spp);
@@ -1248,6 +1543,35 @@ static int render_counter(const bdpt_scene_desc* d, int W, int H, int spp, int m
   return 0;
 }
 
+template <class P>
+static int env_kat(const bdpt_scene_desc* d, int n, const double* u, double* wi, double* pdf, double* rad) {
+  typedef typename P::R R;
+  Scene<R> sc;
+  std::string err;
+  if (!d || !d->envmap || load_scene<R>(d, sc, err)) return BDPT_E_INVALID;
+  for (int k = 0; k < n; k++) {
+    V3<R> w;
+    R p;
+    V3<R> L = env_sample_dir<P>(sc.env, (R)u[4 * k], (R)u[4 * k + 1], (R)u[4 * k + 2], (R)u[4 * k + 3], &w, &p);
+    for (int c = 0; c < 3; c++) { wi[3 * k + c] = w[c]; rad[3 * k + c] = L[c]; }
+    pdf[k] = p;
+  }
+  return 0;
+}
+template <class P>
+static int env_lookup(const bdpt_scene_desc* d, int n, const double* dirs, double* rad, double* pdf) {
+  typedef typename P::R R;
+  Scene<R> sc;
+  std::string err;
+  if (!d || !d->envmap || load_scene<R>(d, sc, err)) return BDPT_E_INVALID;
+  for (int k = 0; k < n; k++) {
+    V3<R> w((R)dirs[3 * k], (R)dirs[3 * k + 1], (R)dirs[3 * k + 2]);
+    V3<R> L = env_radiance<P>(sc.env, w);
+    for (int c = 0; c < 3; c++) rad[3 * k + c] = L[c];
+    pdf[k] = env_pdf_dir<P>(sc.env, w);
+  }
+  return 0;
+}
 }  // namespace orc
 
 using namespace orc;
@@ -1257,13 +1581,16 @@ extern "C" {
 // mode 0: the reference's own sequence (tiles of 32 in raster order, pixels row-major inside a
 // tile, ns_aa samples per pixel; raytraced_renderer.cpp:297-301,610-615); writes eye, light and the
 // reference-ordered sample buffer (all fp64). modes 1/2: counter RNG, samples [s0, s0+count).
-int oracle_render(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode,
-                  uint64_t seed, int s0, int count, int nthreads, double* eye, double* light,
-                  double* sample, double* stats) {
+// rr: Russian roulette (counter modes only, the reference cannot run it; nor an
+// environment light under BDPT, which mode 0 therefore rejects).
+int oracle_render_ex(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode,
+                     uint64_t seed, int s0, int count, int nthreads, double* eye, double* light,
+                     double* sample, double* stats, int rr) {
   if (!d || W <= 0 || H <= 0 || spp <= 0 || max_depth < 0) return BDPT_E_INVALID;
-  if (mode == 1) return render_counter<double>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats);
-  if (mode == 2) return render_counter<float>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats);
+  if (mode == 1) return render_counter<double>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats, rr);
+  if (mode == 2) return render_counter<float>(d, W, H, spp, max_depth, seed, s0, count, nthreads, eye, light, stats, rr);
   if (mode != 0) return BDPT_E_INVALID;
+  if (rr || d->envmap) return BDPT_E_UNSUPPORTED;
   Scene<double> sc;
   std::string err;
   int rc = load_scene<double>(d, sc, err);
@@ -1295,6 +1622,36 @@ int oracle_render(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth
     stats[6] = (double)tr.st.hits; stats[7] = (double)sc.nodes.size();
   }
   return 0;
+}
+
+int oracle_render(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode,
+                  uint64_t seed, int s0, int count, int nthreads, double* eye, double* light,
+                  double* sample, double* stats) {
+  return oracle_render_ex(d, W, H, spp, max_depth, mode, seed, s0, count, nthreads, eye, light, sample, stats, 0);
+}
+
+// Environment-light known answers (tests/test_env.py): the fp64 tables of EnvironmentLight::init
+// (marg[h], cond[w*h], pdf[w*h]); sample_L from explicit uniforms (u = ux, uy, jx, jy) -> wi[3],
+// pdf, radiance[3]; sample_dir / the direction pdf for n directions -> rad[3n], pdf[n]. mode 1:
+// the reference's fp64 libm formulas; mode 2: the device's fp32 semantics.
+int oracle_env_tables(const bdpt_scene_desc* d, double* marg, double* cond, double* pdf) {
+  Scene<double> sc;
+  std::string err;
+  if (!d || !d->envmap || load_scene<double>(d, sc, err)) return BDPT_E_INVALID;
+  const size_t np = (size_t)sc.env.w * sc.env.h;
+  memcpy(marg, sc.env.marg.data(), sc.env.h * sizeof(double));
+  memcpy(cond, sc.env.cond.data(), np * sizeof(double));
+  memcpy(pdf, sc.env.pdf.data(), np * sizeof(double));
+  return 0;
+}
+int oracle_env_sample(const bdpt_scene_desc* d, int mode, int n, const double* u, double* wi, double* pdf,
+                      double* rad) {
+  if (mode == 2) return env_kat<PolicyC32>(d, n, u, wi, pdf, rad);
+  return env_kat<PolicyC64>(d, n, u, wi, pdf, rad);
+}
+int oracle_env_lookup(const bdpt_scene_desc* d, int mode, int n, const double* dirs, double* rad, double* pdf) {
+  if (mode == 2) return env_lookup<PolicyC32>(d, n, dirs, rad, pdf);
+  return env_lookup<PolicyC64>(d, n, dirs, rad, pdf);
 }
 
 // BVH facts of the oracle's reference build: nodes, depth, DFS leaf order (prim indices).

@@ -30,7 +30,7 @@ SRCS := src/pathtracer/bidirection.cpp src/pathtracer/pathtracer.cpp src/pathtra
 SRCS := $(patsubst $(R)/%,%,$(SRCS))
 OBJS := $(addprefix $(OUT)/obj/,$(SRCS:.cpp=.o))
 
-all: $(OUT)/ref_driver
+all: $(OUT)/ref_driver $(OUT)/ref_env_kat
 
 $(OUT)/obj/%.o: $(R)/%.cpp
 	@mkdir -p $(dir $@)
@@ -47,7 +47,19 @@ $(OUT)/obj/ref_driver.o: oracle/ref_driver.cpp
 $(OUT)/ref_driver: $(OBJS) $(OUT)/obj/glew.o $(OUT)/obj/ref_driver.o
 	$(CXX) -o $@ $^ -lGL -lpthread
 
+# environment-light known answers (tests/test_env.py): EnvironmentLight + sampler + tinyexr
+ENV_OBJS := $(addprefix $(OUT)/obj/,src/scene/environment_light.o src/pathtracer/sampler.o CGL/src/lodepng.o \
+            CGL/src/vector2D.o CGL/src/vector3D.o CGL/src/vector4D.o CGL/src/matrix3x3.o CGL/src/matrix4x4.o \
+            CGL/src/color.o CGL/src/complex.o CGL/src/quaternion.o)
+
+$(OUT)/obj/ref_env_kat.o: oracle/ref_env_kat.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OUT)/ref_env_kat: $(ENV_OBJS) $(OUT)/obj/ref_env_kat.o
+	$(CXX) -o $@ $^ -lpthread
+
 clean:
-	rm -rf $(OUT)/obj $(OUT)/ref_driver
+	rm -rf $(OUT)/obj $(OUT)/ref_driver $(OUT)/ref_env_kat
 
 .PHONY: all clean

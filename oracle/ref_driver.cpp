@@ -13,6 +13,11 @@
 //     lights, camera state) as JSON with round-trip (%.17g) doubles,
 //   * BVH statistics and the DFS primitive order of the leaves (bvh.cpp:51-129).
 // These outputs become the golden fixtures under tests/golden/ (see tools/make_golden.py).
+// Options beyond the reference CLI's: -e map.exr loads an environment map exactly as main.cpp's
+// -e (load_exr, restated in oracle/ref_env_kat.cpp's shared copy below); -U swaps the integrator
+// for the reference's unidirectional PathTracer (pathtracer.cpp:47-340; the reference constructs
+// only the BDPT one, raytraced_renderer.cpp:53) with -a batch tol as main.cpp's -a — used as the
+// converged-image cross-check of the environment light (tests/test_env.py).
 
 #include <cstdio>
 #include <cstdlib>
@@ -35,6 +40,9 @@
 #include <unordered_map>
 #include <functional>
 #include <getopt.h>
+
+#define TINYEXR_IMPLEMENTATION
+#include "CGL/tinyexr.h"
 
 // Read-only access to the reference's private state (buffers, camera, BSDF parameters).
 #define private public
@@ -205,12 +213,33 @@ static void dump_scene(const std::string& path, RaytracedRenderer* rr, Camera& c
   o << "]},\n\"prim_order\": [" << porder.str() << "],\n\"triangles\": [\n" << tris.str() << "],\n\"spheres\": [\n" << sphs.str() << "]\n}\n";
 }
 
+// main.cpp:40-77
+static HDRImageBuffer* load_exr(const char* file_path) {
+  const char* err;
+  EXRImage exr;
+  InitEXRImage(&exr);
+  if (ParseMultiChannelEXRHeaderFromFile(&exr, file_path, &err) != 0) return nullptr;
+  for (int i = 0; i < exr.num_channels; i++)
+    if (exr.pixel_types[i] == TINYEXR_PIXELTYPE_HALF) exr.requested_pixel_types[i] = TINYEXR_PIXELTYPE_FLOAT;
+  if (LoadMultiChannelEXRFromFile(&exr, file_path, &err) != 0) return nullptr;
+  HDRImageBuffer* envmap = new HDRImageBuffer();
+  envmap->resize(exr.width, exr.height);
+  float* channel_r = (float*)exr.images[2];
+  float* channel_g = (float*)exr.images[1];
+  float* channel_b = (float*)exr.images[0];
+  for (size_t i = 0; i < (size_t)exr.width * exr.height; i++)
+    envmap->data[i] = Vector3D(channel_r[i], channel_g[i], channel_b[i]);
+  return envmap;
+}
+
 int main(int argc, char** argv) {
-  size_t ns_aa = 1, max_depth = 1, threads = 1, w = 0, h = 0;
+  size_t ns_aa = 1, max_depth = 1, threads = 1, w = 0, h = 0, batch = 32;
+  float tol = 0.05f;
   std::string png = "/dev/null", npy_prefix, scene_json;
-  bool render = true;
+  bool render = true, uni = false;
+  HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:n")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -220,6 +249,9 @@ int main(int argc, char** argv) {
       case 'o': npy_prefix = optarg; break;
       case 'j': scene_json = optarg; break;
       case 'n': render = false; break;
+      case 'e': envmap = load_exr(optarg); if (!envmap) return 4; break;
+      case 'U': uni = true; break;
+      case 'a': batch = atoi(argv[optind - 1]); tol = atof(argv[optind]); optind++; break;   // main.cpp:134-137
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -292,8 +324,17 @@ int main(int argc, char** argv) {
   if (w && h) { screenW = w; screenH = h; camera.set_screen_size(w, h); }
 
   // --- Application ctor (application.cpp:21-40) with AppConfig defaults (application.h:45-65) ---
-  RaytracedRenderer* rr = new RaytracedRenderer(ns_aa, max_depth, 1, 1, 1, 1, threads, 32, 0.05f,
-                                                nullptr, false, "", 0.0, 4.7);
+  RaytracedRenderer* rr = new RaytracedRenderer(ns_aa, max_depth, 1, 1, 1, 1, threads, batch, tol,
+                                                envmap, false, "", 0.0, 4.7);
+  if (uni) {   // the reference's unidirectional integrator with the same settings (:53-74)
+    PathTracer* u = new PathTracer();
+    PathTracer* b = rr->pt;
+    u->ns_aa = b->ns_aa; u->max_ray_depth = b->max_ray_depth; u->ns_area_light = b->ns_area_light;
+    u->ns_diff = b->ns_diff; u->ns_glsy = b->ns_glsy; u->ns_refr = b->ns_refr;
+    u->samplesPerBatch = b->samplesPerBatch; u->maxTolerance = b->maxTolerance;
+    u->direct_hemisphere_sample = b->direct_hemisphere_sample; u->envLight = b->envLight;
+    rr->pt = u;
+  }
   // --- set_up_pathtracer (application.cpp:633-639) ---
   rr->set_camera(&camera);
   rr->set_scene(scene->get_static_scene());
@@ -301,7 +342,9 @@ int main(int argc, char** argv) {
   if (!scene_json.empty()) dump_scene(scene_json, rr, camera);
   if (!render) return 0;
   rr->render_to_file(png, (size_t)-1, 0, 0, 0);
-  if (!npy_prefix.empty()) {
+  if (!npy_prefix.empty() && uni) {
+    write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);
+  } else if (!npy_prefix.empty()) {
     BidirectionalPathTracer* pt = (BidirectionalPathTracer*)rr->pt;
     write_npy(npy_prefix + "_sample.npy", pt->sampleBuffer);
     write_npy(npy_prefix + "_eye.npy", pt->eyeBuffer);

@@ -34,6 +34,10 @@ def oracle():
         P = C.POINTER(C.c_double)
         lib.oracle_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, P, P, P, P]
+        lib.oracle_render_ex.argtypes = lib.oracle_render.argtypes + [C.c_int]
+        lib.oracle_env_tables.argtypes = [C.POINTER(B.SceneDesc), P, P, P]
+        lib.oracle_env_sample.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, P, P, P, P]
+        lib.oracle_env_lookup.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, P, P, P]
         lib.oracle_bvh_info.argtypes = [C.POINTER(B.SceneDesc), C.POINTER(C.c_int),
                                         C.POINTER(C.c_int), C.POINTER(C.c_int)]
         lib.oracle_trace_rays.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.POINTER(C.c_float),
@@ -54,7 +58,8 @@ def _p(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
-def oracle_render(scene, W, H, spp, max_depth, mode, seed=5489, s0=0, count=None, threads=None):
+def oracle_render(scene, W, H, spp, max_depth, mode, seed=5489, s0=0, count=None, threads=None,
+                  rr=False):
     """Returns (sample, eye, light, stats) as float64 arrays (H, W, 3); row 0 = bottom."""
     lib = oracle()
     if count is None:
@@ -66,8 +71,8 @@ def oracle_render(scene, W, H, spp, max_depth, mode, seed=5489, s0=0, count=None
     samp = np.zeros((H, W, 3))
     st = np.zeros(8)
     d = scene.desc()
-    rc = lib.oracle_render(C.byref(d), W, H, spp, max_depth, mode, seed, s0, count, threads,
-                           _p(eye), _p(light), _p(samp), _p(st))
+    rc = lib.oracle_render_ex(C.byref(d), W, H, spp, max_depth, mode, seed, s0, count, threads,
+                              _p(eye), _p(light), _p(samp), _p(st), 1 if rr else 0)
     if rc != 0:
         raise RuntimeError(f"oracle_render rc={rc}")
     if mode != MODE_REF:

@@ -18,9 +18,9 @@ struct HostSink {
   }
 };
 
-template <int MAXV, int LM>
+template <int MAXV, int LM, bool EXT>
 static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed, int s0, int count,
-               const int* pixels, int npix, double* eye, double* light, double* stats) {
+               const int* pixels, int npix, double* eye, double* light, double* stats, int rr) {
   SceneView S;
   const HostBvh& T = hs.tree(lm_width(LM));
   S.nodes = (const float4*)T.nodes.data();
@@ -35,8 +35,19 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.lgeom = LM == 1 ? S.geom : nullptr;
   S.ntop = 0;
   S.cam = hs.cam;
+  const size_t np = (size_t)hs.env_w * hs.env_h;
+  S.env.light = hs.env_light;
+  S.env.w = hs.env_w;
+  S.env.h = hs.env_h;
+  S.env.marg = hs.env.data();
+  S.env.cond = hs.env.data() + hs.env_h;
+  S.env.pdf = hs.env.data() + hs.env_h + np;
+  S.env.rgb = hs.env.data() + hs.env_h + 2 * np;
+  S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];
+  S.env.rad = hs.env_rad;
   SampleParams sp;
   sp.W = W; sp.H = H; sp.spp = spp; sp.max_depth = M; sp.seed = seed;
+  sp.rr = rr;
   std::vector<double> lb((size_t)W * H * 3, 0.0);
   HostSink sink{&lb, W};
   Counters cnt = {0, 0, 0, 0, 0, 0};
@@ -46,7 +57,7 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   for (int q = 0; q < total; q++) {
     int x = pixels ? pixels[2 * q] : q % W, y = pixels ? pixels[2 * q + 1] : q / W;
     for (int s = s0; s < s0 + count; s++) {
-      f3 v = render_sample<MAXV, LM>(S, sp, *P, cnt, x, y, (uint32_t)s, sink);
+      f3 v = render_sample<MAXV, LM, EXT>(S, sp, *P, cnt, x, y, (uint32_t)s, sink);
       size_t k = 3 * ((size_t)x + (size_t)y * W);
       eye[k] += (double)(v.x * inv); eye[k + 1] += (double)(v.y * inv); eye[k + 2] += (double)(v.z * inv);
     }
@@ -60,26 +71,35 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   return 0;
 }
 
+template <int LM, bool EXT>
+static int render_maxv(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed, int s0, int count,
+                       const int* pixels, int npix, double* eye, double* light, double* stats, int rr) {
+  int need = M < 1 ? 1 : M;
+  if (need <= 5) return run<5, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  if (need <= 8) return run<8, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  if (need <= 16) return run<16, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  return BDPT_E_UNSUPPORTED;
+}
+
 template <int LM>
 static int render_lm(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
-                     int count, const int* pixels, int npix, double* eye, double* light, double* stats) {
+                     int count, const int* pixels, int npix, double* eye, double* light, double* stats, int rr) {
   HostScene hs;
   std::string err;
   int rc = build_host_scene(d, hs, err);
   if (rc) { fprintf(stderr, "core_cpu: %s\n", err.c_str()); return rc; }
-  int need = M < 1 ? 1 : M;
-  if (need <= 5) return run<5, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  if (need <= 8) return run<8, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  if (need <= 16) return run<16, LM>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  return BDPT_E_UNSUPPORTED;
+  // the kernel selection of bdpt_create: EXT kernels for an environment light or roulette
+  if (hs.env_light >= 0 || rr)
+    return render_maxv<LM, true>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  return render_maxv<LM, false>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
 }
 
 // lds_mode 0: the HBM tree (lm_width(0) children per node); 1: the LDS-mode tree (lm_width(1))
 extern "C" int core_cpu_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
                                int count, const int* pixels, int npix, double* eye, double* light, double* stats,
-                               int lds_mode) {
-  if (lds_mode == 1) return render_lm<1>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
-  return render_lm<0>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats);
+                               int lds_mode, int rr) {
+  if (lds_mode == 1) return render_lm<1>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  return render_lm<0>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
 }
 
 extern "C" int core_cpu_scene_info(const bdpt_scene_desc* d, int* depth, int* ref_nodes, int* prim_ref) {

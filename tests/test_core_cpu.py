@@ -25,14 +25,14 @@ def core():
         P = C.POINTER(C.c_double)
         lib.core_cpu_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int,
-                                        P, P, P, C.c_int]
+                                        P, P, P, C.c_int, C.c_int]
         lib.core_cpu_scene_info.argtypes = [C.POINTER(B.SceneDesc), C.POINTER(C.c_int),
                                             C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _core = lib
     return _core
 
 
-def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None, lds_mode=0):
+def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None, lds_mode=0, rr=False):
     lib = core()
     count = spp - s0 if count is None else count
     eye = np.zeros((H, W, 3))
@@ -41,7 +41,8 @@ def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None, lds_mode=0):
     d = scene.desc()
     pd = C.POINTER(C.c_double)
     rc = lib.core_cpu_render(C.byref(d), W, H, spp, M, seed, s0, count, None, 0,
-                             eye.ctypes.data_as(pd), light.ctypes.data_as(pd), st.ctypes.data_as(pd), lds_mode)
+                             eye.ctypes.data_as(pd), light.ctypes.data_as(pd), st.ctypes.data_as(pd), lds_mode,
+                             1 if rr else 0)
     assert rc == 0
     return eye, light, st
 
@@ -58,6 +59,28 @@ def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M, lds_mode)
     sc = golden_scene(name, W, H)
     eye, light, st = core_render(sc, W, H, spp, M, seed=1234, lds_mode=lds_mode)
     _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=1234, threads=1)
+    assert np.isfinite(eye).all() and np.isfinite(light).all()
+    assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
+    assert np.array_equal(light, olight), f"light max diff {np.abs(light - olight).max()}"
+
+
+EXT_CASES = [("CBspheres_lambertian", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 5, False, True),
+             ("CBempty", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 8, True, False),
+             ("CBgems", 32, 24, 1, 7, True, True), ("CBspheres_lambertian", 24, 18, 2, 8, True, True)]
+
+
+@pytest.mark.parametrize("lds_mode", [0, 1])
+@pytest.mark.parametrize("name,W,H,spp,M,rr,env", EXT_CASES)
+def test_device_pipeline_bit_exact_env_rr(name, W, H, spp, M, rr, env, lds_mode):
+    """The EXT kernels' code (environment light, Russian roulette) vs mode 2."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from envmap import synth_envmap
+    sc = golden_scene(name, W, H)
+    if env:
+        sc.set_envmap(synth_envmap(32, 16))
+    eye, light, st = core_render(sc, W, H, spp, M, seed=99, lds_mode=lds_mode, rr=rr)
+    _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=99, threads=1, rr=rr)
     assert np.isfinite(eye).all() and np.isfinite(light).all()
     assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
     assert np.array_equal(light, olight), f"light max diff {np.abs(light - olight).max()}"

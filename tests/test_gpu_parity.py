@@ -21,9 +21,9 @@ PIPES = [pytest.param(B.PIPELINE_MEGAKERNEL, id="mega"), pytest.param(B.PIPELINE
 
 
 def _gpu_render(sc, W, H, S, M, seed=5489, tiles=(), ranges=None, spl=0, stats=False,
-                pipeline=B.PIPELINE_AUTO):
+                pipeline=B.PIPELINE_AUTO, rr=False):
     pt = B.BidirectionalPathTracer(sc, W, H, S, M, seed=seed, samples_per_lane=spl,
-                                   collect_stats=stats, pipeline=pipeline)
+                                   collect_stats=stats, pipeline=pipeline, russian_roulette=rr)
     try:
         if ranges is None:
             ranges = [(0, S)]
@@ -146,3 +146,48 @@ def test_pipelines_agree():
     a = _gpu_render(sc, W, H, S, M, pipeline=B.PIPELINE_MEGAKERNEL)
     b = _gpu_render(sc, W, H, S, M, pipeline=B.PIPELINE_WAVEFRONT)
     assert _rmse(a["sample"], b["sample"]) < 1e-6
+
+
+# --- environment light + Russian roulette: the EXT kernels -----------------------
+def _with_env(sc, w=64, h=32):
+    import os
+    import sys
+    from _util import REPO
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from envmap import synth_envmap
+    sc.set_envmap(synth_envmap(w, h))
+    return sc
+
+
+@pytest.mark.parametrize("lds", ["0", "1", "2"])
+@pytest.mark.parametrize("name,W,H,S,M,rr,env", [
+    ("CBspheres_lambertian", 128, 96, 4, 5, False, True),
+    ("CBspheres", 128, 96, 4, 8, True, True),
+    ("CBgems", 128, 96, 2, 7, True, False),
+    ("CBempty", 96, 72, 4, 5, True, True),
+])
+def test_parity_env_rr_vs_oracle(name, W, H, S, M, rr, env, lds, monkeypatch):
+    """EXT megakernel (every LDS mode: scene in HBM, whole scene in LDS, BFS treelet) vs mode 2."""
+    monkeypatch.setenv("BDPT_LDS_MODE", lds)
+    sc = golden_scene(name, W, H)
+    if env:
+        _with_env(sc)
+    g = _gpu_render(sc, W, H, S, M, rr=rr)
+    samp, eye, light, st = oracle_render(sc, W, H, S, M, MODE_C32, rr=rr)
+    assert np.isfinite(g["sample"]).all()
+    r = _rmse(g["sample"], samp)
+    print(f"EXT {name} {W}x{H} s{S} m{M} rr={rr} env={env} lds={lds}: rmse {r:.3e} "
+          f"mean gpu {g['sample'].mean():.6f} oracle {samp.mean():.6f}")
+    assert r < RMSE_TOL and _rmse(g["eye"], eye) < RMSE_TOL and _rmse(g["light"], light) < RMSE_TOL
+
+
+def test_parity_env_only_scene():
+    """The environment as the only light (no area light in the scene)."""
+    import os
+    from _util import REPO
+    env = os.path.join(REPO, "tests", "golden", "env")
+    sc = B.load_dae(os.path.join(env, "CBspheres_envonly.dae"), 96, 72)
+    sc.set_envmap(B.load_exr(os.path.join(env, "sky_32x16_zip_half.exr")))
+    g = _gpu_render(sc, 96, 72, 4, 12, rr=True)
+    samp = oracle_render(sc, 96, 72, 4, 12, MODE_C32, rr=True)[0]
+    assert _rmse(g["sample"], samp) < RMSE_TOL
