@@ -42,7 +42,7 @@ def algorithmic_bytes(st) -> int:
             + BYTES_HIT * st.hits)
 
 
-def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0) -> dict:
+def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0, rr: bool = False) -> dict:
     """The oracle's fp64 reference-semantics path (mode COUNTER64: the reference's arithmetic,
     multi-threaded like the reference's -t N) timed on this host on a bounded sample of the same
     workload (full 480x360 frame, a few spp)."""
@@ -51,7 +51,7 @@ def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0) -> dict
     s0 = 0
     while t_tot < budget_s * 0.8 and s0 < SPP:
         t0 = time.perf_counter()
-        oracle_render(scene, W, H, SPP, M, MODE_C64, seed=5489, s0=s0, count=spp_run, threads=threads)
+        oracle_render(scene, W, H, SPP, M, MODE_C64, seed=5489, s0=s0, count=spp_run, threads=threads, rr=rr)
         dt = time.perf_counter() - t0
         t_tot += dt
         done += W * H * spp_run
@@ -98,19 +98,19 @@ def cpu_baseline_reference(dae: str, name: str, threads: int, budget_s: float = 
                       f"{t_tot:.1f} s of rendering"}
 
 
-def parity_check(scene, seed: int) -> dict:
+def parity_check(scene, seed: int, rr: bool = False) -> dict:
     """Per-pixel RMSE of the GPU sample buffer vs the oracle's COUNTER32 CPU path, same seed,
     same workload at 2 spp (the CPU side of the metric)."""
     import numpy as np
     import bdpt_amd as B
     from _util import MODE_C32, oracle_render
     S = 2
-    pt = B.BidirectionalPathTracer(scene, W, H, S, M, seed=seed)
+    pt = B.BidirectionalPathTracer(scene, W, H, S, M, seed=seed, russian_roulette=rr)
     pt.raytrace_tiles()
     g = pt.read_frame(B.FRAME_SAMPLE).astype(np.float64)
     pt.close()
     ref = oracle_render(scene, W, H, S, M, MODE_C32, seed=seed,
-                        threads=min(16, os.cpu_count() or 1))[0]
+                        threads=min(16, os.cpu_count() or 1), rr=rr)[0]
     return {"rmse": float(np.sqrt(np.mean((g - ref) ** 2))), "spp": S, "tolerance": 1e-4,
             "cpu": "oracle COUNTER32 (fp32 device semantics)"}
 
@@ -131,6 +131,10 @@ def main() -> int:
     ap.add_argument("--spp", type=int, default=SPP)
     ap.add_argument("--max-depth", type=int, default=M)
     ap.add_argument("--pipeline", type=int, default=0, help="0 auto, 1 megakernel, 2 wavefront")
+    ap.add_argument("--envmap", default=None,
+                    help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
+                         "synthetic sky of tools/envmap.py (the reference's exr/*.exr are LFS pointers)")
+    ap.add_argument("--rr", action="store_true", help="Russian roulette on both subpaths")
     args = ap.parse_args()
     W, H, SPP, M = args.width, args.height, args.spp, args.max_depth
 
@@ -153,12 +157,23 @@ def main() -> int:
 
     scene = (B.load_dae(args.scene, W, H) if args.scene.endswith(".dae")
              else golden_scene(args.scene, W, H))
+    env_desc = None
+    if args.envmap:
+        if args.envmap.startswith("synth:"):
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from envmap import synth_envmap
+            ew, eh = (int(v) for v in args.envmap[6:].split("x"))
+            scene.set_envmap(synth_envmap(ew, eh))
+            env_desc = f"synthetic sky {ew}x{eh} (tools/envmap.py)"
+        else:
+            scene.set_envmap(B.load_exr(args.envmap))
+            env_desc = os.path.basename(args.envmap)
     seed = 5489
     stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
     torch.cuda.set_stream(stream)
     # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
     pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                   pipeline=args.pipeline)
+                                   pipeline=args.pipeline, russian_roulette=args.rr)
     pt.set_stream(stream.cuda_stream)
     frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
 
@@ -201,7 +216,7 @@ def main() -> int:
     # algorithmic bytes of one launch: in-kernel counters on a separate, untimed launch of the
     # same workload (counting perturbs timing), SURVEY.md §8d.
     ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                   collect_stats=True, pipeline=args.pipeline)
+                                   collect_stats=True, pipeline=args.pipeline, russian_roulette=args.rr)
     ps.raytrace_tiles([], rank * SPP, SPP)
     st = ps.stats()
     ps.close()
@@ -211,7 +226,7 @@ def main() -> int:
     samples_total = W * H * SPP * world * args.steps
     value = samples_total / elapsed / 1e6
     traffic = None
-    default_workload = (args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5)
+    default_workload = (args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5) and not args.envmap and not args.rr
     tpath = os.path.join(REPO, "profiles", "traffic_r01.json")   # PMC pass of this workload
     if default_workload and os.path.exists(tpath):
         with open(tpath) as f:
@@ -236,11 +251,13 @@ def main() -> int:
         "data": f"synthetic: fixed-seed renders (Philox counter RNG) of the reference's scene "
                 f"{os.path.basename(args.scene)} as the reference loads it",
         "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} -s {SPP} -m {M}"
+                               f"{' + env ' + env_desc if env_desc else ''}{' RR on' if args.rr else ''}"
                                f"{' (BASELINE configs[1])' if default_workload else ''} "
                                f"per GPU, sample-range shards + RCCL sum-reduce",
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
                    "scene": args.scene, "width": W, "height": H, "spp_per_gpu": SPP,
-                   "max_depth": M, "parallelism": f"samples x{world}"},
+                   "max_depth": M, "envmap": env_desc, "russian_roulette": args.rr,
+                   "parallelism": f"samples x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                      "traffic": traffic, "kernel": "k_bdpt_sample", "kernel_ms": round(kern_ms, 3),
@@ -251,12 +268,14 @@ def main() -> int:
                                            "shadow_rays": st.shadow_rays}},
     }
     if world == 1 and not args.no_parity:
-        out["parity"] = parity_check(scene, seed)
+        out["parity"] = parity_check(scene, seed, rr=args.rr)
     if world == 1 and not args.no_cpu_baseline:
         thr = min(16, os.cpu_count() or 1)
         dae = args.scene if args.scene.endswith(".dae") else os.path.join(REPO, "scenes", args.scene + ".dae")
-        port = cpu_baseline(scene, args.scene, threads=thr)
-        ref = cpu_baseline_reference(dae, os.path.basename(args.scene), threads=thr)
+        port = cpu_baseline(scene, args.scene, threads=thr, rr=args.rr)
+        # the reference cannot run the environment light / roulette under BDPT: port only
+        ref = (None if (args.envmap or args.rr)
+               else cpu_baseline_reference(dae, os.path.basename(args.scene), threads=thr))
         out["cpu_baseline"] = ref if ref is not None else port
         if ref is not None:   # the oracle port's fp64 path, same host, for comparison
             out["cpu_baseline"]["port"] = {"value": port["value"], "cores": port["cores"], "sample": port["sample"]}

@@ -2,11 +2,13 @@
 // in windowless mode, rendering through libbdpt_amd.so on MI355X GPUs.
 //
 //   pathtracer [-s spp] [-m max_depth] [-r W H] [-f out.png] [-p x y dx dy] [-t threads]
-//              [-l n] [-g gpus] [-S seed] [--dump-scene scene.json] scene.dae
+//              [-l n] [-e envmap.exr] [--rr] [-g gpus] [-S seed] [--dump-scene scene.json] scene.dae
 //
 // Same flags and defaults as the reference (-s 1, -m 1, 800x600 when -r is absent; -t / -l are
 // accepted and do not apply to the GPU path; -p renders one cell). -g N splits the sample range
-// over N devices (one context and one host thread per device) and sums the frames.
+// over N devices (one context and one host thread per device) and sums the frames. -e loads an
+// environment map as the reference's -e does (load_exr, main.cpp:115-119) — under BDPT, which the
+// reference cannot run with it; --rr turns on Russian roulette (bidirection.cpp:87-93).
 // Output: the tonemapped PNG and the "_rate.png" sampling-rate image, as render_to_file writes
 // them (raytraced_renderer.cpp:330-347, 690-761).
 #include <chrono>
@@ -29,6 +31,8 @@ void usage(const char* b) {
   printf("  -l  <INT>        Number of samples per area light (unused by BDPT)\n");
   printf("  -t  <INT>        Number of render threads (GPU path: ignored)\n");
   printf("  -m  <INT>        Maximum ray depth\n");
+  printf("  -e  <PATH>       Path to environment map\n");
+  printf("  --rr             Russian roulette on both subpaths\n");
   printf("  -f  <FILENAME>   Image (.png) file to save output to\n");
   printf("  -r  <INT> <INT>  Width and height of output image\n");
   printf("  -p  <x> <y> <dx> <dy>  Render only this cell\n");
@@ -51,7 +55,8 @@ int main(int argc, char** argv) {
   int spp = 1, max_depth = 1, w = 0, h = 0, gpus = 1;
   long cx = -1, cy = 0, cdx = 0, cdy = 0;
   unsigned long long seed = 5489;
-  std::string out, dump, scene;
+  std::string out, dump, scene, envpath;
+  bool rr = false;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto need = [&](int n) {
@@ -66,6 +71,8 @@ int main(int argc, char** argv) {
     else if (a == "-g") { need(1); gpus = atoi(argv[++i]); }
     else if (a == "-S") { need(1); seed = strtoull(argv[++i], nullptr, 10); }
     else if (a == "--dump-scene") { need(1); dump = argv[++i]; }
+    else if (a == "-e") { need(1); envpath = argv[++i]; }
+    else if (a == "--rr") rr = true;
     else if (a == "--tonemap") {
       need(4);
       const int tw = atoi(argv[i + 2]), tht = atoi(argv[i + 3]);
@@ -80,7 +87,7 @@ int main(int argc, char** argv) {
       if (!bdpt::write_png(o, bdpt::tonemap(hdr.data(), tw, tht), tw, tht)) return 1;
       return bdpt::write_rate_png(o, std::vector<float>((size_t)tw * tht, 1.0f), tw, tht) ? 0 : 1;
     }
-    else if (a == "-e" || a == "-c" || a == "-b" || a == "-d") {
+    else if (a == "-c" || a == "-b" || a == "-d") {
       fprintf(stderr, "[PathTracer] option %s is not supported by the BDPT GPU path\n", a.c_str());
       return 1;
     } else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
@@ -99,6 +106,14 @@ int main(int argc, char** argv) {
   if (w <= 0 || h <= 0) { w = 800; h = 600; }
   bdpt_scene_desc desc;
   bdpt_dae_get_desc(dae, &desc);
+  bdpt_envmap env;
+  float* env_rgb = nullptr;
+  if (!envpath.empty()) {
+    fprintf(stderr, "[PathTracer] Loading environment map %s\n", envpath.c_str());
+    if (bdpt_exr_load(envpath.c_str(), &env.width, &env.height, &env_rgb) != BDPT_OK) return fail("loading environment map");
+    env.rgb = env_rgb;
+    desc.envmap = &env;
+  }
   fprintf(stderr, "[PathTracer] %d primitives, %d materials, %d lights; %dx%d, %d spp, max depth %d, %d GPU(s)\n",
           desc.nprim, desc.nmat, desc.nlight, w, h, spp, max_depth, gpus);
 
@@ -114,6 +129,7 @@ int main(int argc, char** argv) {
       bdpt_params p;
       memset(&p, 0, sizeof p);
       p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed; p.device = g;
+      p.russian_roulette = rr ? 1 : 0;
       void* ctx = nullptr;
       const int s0 = (int)((long long)spp * g / gpus), s1 = (int)((long long)spp * (g + 1) / gpus);
       int rc = bdpt_create(&desc, &p, &ctx);
@@ -131,6 +147,7 @@ int main(int argc, char** argv) {
     if (rcs[g] != BDPT_OK) {
       fprintf(stderr, "[PathTracer] GPU %d: %s\n", g, errs[g].c_str());
       bdpt_dae_free(dae);
+      bdpt_exr_free(env_rgb);
       return 1;
     }
   std::vector<float>& img = frames[0];
@@ -153,5 +170,6 @@ int main(int argc, char** argv) {
   bdpt::write_rate_png(out, rate, w, h);
   fprintf(stdout, "[PathTracer] Job completed.\n");
   bdpt_dae_free(dae);
+  bdpt_exr_free(env_rgb);
   return 0;
 }

@@ -44,3 +44,27 @@ def test_cli_cell_render(tmp_path):
     inside = img[8:20, 16:36, :3].astype(int).sum()
     outside = img[:, :, :3].astype(int).sum() - inside
     assert inside > 0 and outside < inside           # only splats may land outside the cell
+
+
+def test_cli_environment_map_and_roulette(tmp_path):
+    """-e map.exr (the reference's flag, load_exr) + --rr on the environment-only scene, against the
+    oracle's COUNTER32 render of the same inputs through the same output stage."""
+    import bdpt_amd as B
+    env = os.path.join(REPO, "tests", "golden", "env")
+    W, H, S, M = 64, 48, 2, 8
+    out = tmp_path / "env.png"
+    dae = os.path.join(env, "CBspheres_envonly.dae")
+    exr = os.path.join(env, "sky_32x16_zip_half.exr")
+    r = subprocess.run([CLI, "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-e", exr, "--rr", "-f",
+                        str(out), dae], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ours = read_png(out)
+    sc = B.load_dae(dae, W, H)
+    sc.set_envmap(B.load_exr(exr))
+    ref_hdr = oracle_render(sc, W, H, S, M, MODE_C32, rr=True)[0]
+    raw = tmp_path / "ref.f64"
+    np.ascontiguousarray(ref_hdr, dtype="<f8").tofile(raw)
+    subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
+    ref = read_png(tmp_path / "ref.png")
+    d = np.abs(ours.astype(int) - ref.astype(int))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
