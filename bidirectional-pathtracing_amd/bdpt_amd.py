@@ -69,7 +69,14 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
                 ("max_depth", C.c_int32), ("seed", C.c_uint64), ("samples_per_lane", C.c_int32),
                 ("device", C.c_int32), ("collect_stats", C.c_int32), ("pipeline", C.c_int32),
-                ("russian_roulette", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("russian_roulette", C.c_int32), ("integrator", C.c_int32),
+                ("ns_area_light", C.c_int32), ("samples_per_batch", C.c_int32),
+                ("max_tolerance", C.c_float), ("direct_hemisphere_sample", C.c_int32),
+                ("lens_radius", C.c_double), ("focal_distance", C.c_double),
+                ("reserved", C.c_int32 * 4)]
+
+
+INTEGRATOR_BDPT, INTEGRATOR_PT = 0, 1
 
 
 class Tile(C.Structure):
@@ -186,6 +193,8 @@ def scene_from_json(js) -> Scene:
         elif m["type"] == "refraction":
             M.b[:] = m["transmittance"]
             M.ior, M.roughness = m["ior"], m.get("roughness", 0.0)
+        elif m["type"] == "microfacet" and "eta" in m:
+            M.a[:], M.b[:], M.roughness = m["eta"], m["k"], m["alpha"]
         mats.append(M)
     lights = []
     for l in js["lights"]:
@@ -285,6 +294,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_frame_device_ptr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
     lib.bdpt_copy_frame.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.bdpt_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    lib.bdpt_read_sample_counts.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
     lib.bdpt_trace_rays.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.c_int32,
                                     C.POINTER(C.c_float), C.POINTER(C.c_int32)]
     lib.bdpt_dae_load.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
@@ -318,7 +328,7 @@ class BidirectionalPathTracer:
     def __init__(self, scene: Scene, width: int, height: int, spp: int, max_depth: int,
                  seed: int = 5489, device: int = 0, samples_per_lane: int = 0,
                  collect_stats: bool = False, pipeline: int = PIPELINE_AUTO,
-                 russian_roulette: bool = False):
+                 russian_roulette: bool = False, _pt: Optional[dict] = None):
         self.lib = load_library()
         self.scene = scene
         self.width, self.height, self.spp, self.max_depth = width, height, spp, max_depth
@@ -328,6 +338,13 @@ class BidirectionalPathTracer:
         p.collect_stats = 1 if collect_stats else 0
         p.pipeline = pipeline
         p.russian_roulette = 1 if russian_roulette else 0
+        if _pt is not None:
+            p.integrator = INTEGRATOR_PT
+            p.ns_area_light = _pt["ns_area_light"]
+            p.samples_per_batch = _pt["samples_per_batch"]
+            p.max_tolerance = _pt["max_tolerance"]
+            p.direct_hemisphere_sample = 1 if _pt["direct_hemisphere_sample"] else 0
+            p.lens_radius, p.focal_distance = _pt["lens_radius"], _pt["focal_distance"]
         self._desc = scene.desc()
         ctx = C.c_void_p()
         _check(self.lib.bdpt_create(C.byref(self._desc), C.byref(p), C.byref(ctx)), self.lib)
@@ -382,6 +399,13 @@ class BidirectionalPathTracer:
     def copy_frame(self, which: int, dst_device_ptr: int) -> None:
         _check(self.lib.bdpt_copy_frame(self.ctx, which, C.c_void_p(dst_device_ptr)), self.lib)
 
+    def read_sample_counts(self) -> np.ndarray:
+        """sampleCountBuffer (pathtracer.h:94): (H, W) int32, row 0 = bottom."""
+        out = np.empty((self.height, self.width), dtype=np.int32)
+        _check(self.lib.bdpt_read_sample_counts(self.ctx, out.ctypes.data_as(C.POINTER(C.c_int32))),
+               self.lib)
+        return out
+
     def stats(self) -> Stats:
         s = Stats()
         _check(self.lib.bdpt_get_stats(self.ctx, C.byref(s)), self.lib)
@@ -396,3 +420,23 @@ class BidirectionalPathTracer:
                                         1 if any_hit else 0, t.ctypes.data_as(C.POINTER(C.c_float)),
                                         prim.ctypes.data_as(C.POINTER(C.c_int32))), self.lib)
         return t, prim
+
+
+class PathTracer(BidirectionalPathTracer):
+    """The reference's unidirectional integrator (PathTracer, pathtracer.cpp:47-340) on the GPU:
+    next-event estimation (-l samples per area light, or -H hemisphere sampling), adaptive
+    sampling in batches (-a batch tol), thin lens (-b, -d), roulette at max_depth 0, the
+    environment light, MicrofacetBSDF. Defaults are AppConfig's (application.h:45-65).
+    raytrace_tiles() renders whole pixels (spp_begin 0, all ns_aa samples)."""
+
+    def __init__(self, scene: Scene, width: int, height: int, spp: int, max_depth: int,
+                 seed: int = 5489, device: int = 0, ns_area_light: int = 1,
+                 samples_per_batch: int = 32, max_tolerance: float = 0.05,
+                 direct_hemisphere_sample: bool = False, lens_radius: float = 0.0,
+                 focal_distance: float = 4.7, collect_stats: bool = False):
+        super().__init__(scene, width, height, spp, max_depth, seed=seed, device=device,
+                         collect_stats=collect_stats,
+                         _pt=dict(ns_area_light=ns_area_light, samples_per_batch=samples_per_batch,
+                                  max_tolerance=max_tolerance,
+                                  direct_hemisphere_sample=direct_hemisphere_sample,
+                                  lens_radius=lens_radius, focal_distance=focal_distance))

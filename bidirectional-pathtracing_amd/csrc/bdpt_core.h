@@ -193,7 +193,7 @@ BDPT_HD int lround_pos(float x) {
 
 // ------------------------------------------------------------------------------------------------
 // Scene layout in HBM (see DESIGN.md §Data layout)
-enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REFRACTION = 4 };
+enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REFRACTION = 4, MAT_MICROFACET = 5 };
 // Vtx::mat of a vertex without BSDF: -1 camera / area or point light vertex, MAT_ENV_V a vertex
 // of the environment light (an escaped eye ray, or an env light subpath's first vertex).
 enum { MAT_ENV_V = -2 };
@@ -204,9 +204,10 @@ enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2 };
 
 struct DMat {
   int type;
-  float a[3];
-  float b[3];
+  float a[3];    // microfacet: eta
+  float b[3];    // microfacet: k
   float ior;
+  float alpha;   // microfacet roughness (PathTracer only: BDPT rejects microfacet)
 };
 struct DLight {
   int type;
@@ -764,9 +765,71 @@ BDPT_HD bool refract_dir(f3 wo, f3* wi, float ior) {   // advanced_bsdf.cpp:279-
   return true;
 }
 
+// MicrofacetBSDF (advanced_bsdf.cpp:46-142, bsdf.h:176-184) in the device semantics (PathTracer
+// only): cos(acos z) = z, tan(acos z) = sqrt(1 - z^2) / z, integer powers by products, erf / exp /
+// log from the fp32 math library (oracle mode 2 restates it, oracle/bdpt_oracle.cpp mf_*).
+BDPT_HD float mf_lambda(float alpha, f3 w) {
+  const float c = fminf(fmaxf(w.z, (float)(-1.0 + 1e-5)), (float)(1.0 - 1e-5));
+  const float t = sqrtf(1.0f - c * c) / c;
+  const float a = 1.0f / (alpha * t);
+  return 0.5f * (erff(a) - 1.0f + expf(-a * a) / (a * BDPT_PI_F));
+}
+BDPT_HD float mf_G(float alpha, f3 wo, f3 wi) { return 1.0f / (1.0f + mf_lambda(alpha, wi) + mf_lambda(alpha, wo)); }
+BDPT_HD float mf_D(float alpha, f3 h) {
+  const float c = h.z;
+  const float t = sqrtf(fmaxf(0.0f, 1.0f - c * c)) / c;
+  const float q = t / alpha;
+  const float c2 = c * c;
+  return expf(-(q * q)) / (BDPT_PI_F * alpha * alpha * (c2 * c2));
+}
+BDPT_HD f3 mf_F(const DMat& M, f3 wi) {   // (Rs + Rp) / 2, CGL operator order
+  const f3 eta = mk3(M.a[0], M.a[1], M.a[2]), k = mk3(M.b[0], M.b[1], M.b[2]);
+  const float c = fabsf(wi.z) / norm(wi);
+  const float c2 = c * c;
+  const f3 e2k2 = add(mul(eta, eta), mul(k, k));
+  const f3 t = muls(smul(2.0f, eta), c);
+  const f3 Rs = mk3((e2k2.x - t.x + c2) / (e2k2.x + t.x + c2), (e2k2.y - t.y + c2) / (e2k2.y + t.y + c2),
+                    (e2k2.z - t.z + c2) / (e2k2.z + t.z + c2));
+  const f3 e = muls(e2k2, c2);
+  const f3 Rp = mk3((e.x - t.x + 1.0f) / (e.x + t.x + 1.0f), (e.y - t.y + 1.0f) / (e.y + t.y + 1.0f),
+                    (e.z - t.z + 1.0f) / (e.z + t.z + 1.0f));
+  return divs(add(Rs, Rp), 2.0f);
+}
+BDPT_HD f3 mf_f(const DMat& M, f3 wo, f3 wi) {
+  if (wo.z <= BDPT_EPS_F || wi.z <= BDPT_EPS_F) return splat3(0);
+  const f3 h = normalize(add(wo, wi));
+  return divs(muls(muls(mf_F(M, wi), mf_G(M.alpha, wo, wi)), mf_D(M.alpha, h)), 4.0f * wo.z * wi.z);
+}
+BDPT_HD f3 mf_sample_f(const DMat& M, Rng& g, f3 wo, f3* wi, float* pdf) {
+  float rx, ry;
+  grid2d(g, &rx, &ry);
+  const float alpha = M.alpha;
+  const float tt = sqrtf(-alpha * alpha * logf(1.0f - rx));   // tan(theta)
+  const float ct = 1.0f / sqrtf(1.0f + tt * tt);
+  const float st = tt * ct;
+  float cp, sp;
+  cos_sin_2pi(ry, &cp, &sp);
+  const f3 h = mk3(st * cp, st * sp, ct);
+  const float costheta = dot(wo, h) / norm(wo);
+  const f3 d = sub(wo, muls(muls(h, costheta), norm(wo)));
+  *wi = normalize(sub(muls(muls(h, costheta), norm(wo)), d));
+  if (wo.z <= BDPT_EPS_F || wi->z <= BDPT_EPS_F) {
+    *pdf = 1;
+    *wi = mk3(0, 0, 1);
+    return splat3(0);
+  }
+  const float q = tt / alpha, c2 = ct * ct;
+  const float p_theta = 2.0f * st * expf(-(q * q)) / (alpha * alpha * (c2 * ct));
+  const float p_phi = 1.0f / (2.0f * BDPT_PI_F);
+  const float pdf_h = p_theta * p_phi / st;
+  *pdf = pdf_h / (4.0f * dot(*wi, h));
+  return mf_f(M, wo, *wi);
+}
+
 BDPT_HD f3 sample_f(const DMat& M, Rng& g, f3 wo, f3* wi, float* pdf) {
   f3 A = mk3(M.a[0], M.a[1], M.a[2]);
   switch (M.type) {
+    case MAT_MICROFACET: return mf_sample_f(M, g, wo, wi, pdf);
     case MAT_DIFFUSE: {
       *wi = cosine_hemi(g, pdf);
       if (wo.z < 0 || wi->z < 0) return splat3(0);
@@ -1610,6 +1673,209 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
     }
   }
   return eye_sum;
+}
+
+// ================================================================================================
+// The unidirectional PathTracer (pathtracer.cpp:47-340) in the device
+// semantics. The reference recurses (at_least_one_bounce, :181-262) and adds each vertex's
+// continuation after the deeper vertices return; the walk here runs forward and keeps what each
+// vertex contributes (NEE, f, cos, pdf, the next hit's emission), then folds innermost-first so the
+// fp32 operation order is the reference's (oracle mode 2 runs the recursion itself, bit-exact).
+struct PtParams {
+  int W, H, spp, max_depth;   // max_depth 0: roulette (coin_flip(0.3), depth < 20)
+  uint64_t seed;
+  int ns_area_light, batch, hemisphere;
+  float tol;                  // maxTolerance (adaptive sampling, :320-334)
+  float lens_radius, focal_distance;
+};
+constexpr int kPtMaxVerts = 21;   // depths 0..20 (the roulette cap, :215)
+
+BDPT_HD bool mat_is_delta(const SceneView& S, int m) { return is_delta(S.mats[m].type); }
+BDPT_HD f3 mat_emission(const SceneView& S, int m) {
+  const DMat& M = S.mats[m];
+  return M.type == MAT_EMISSION ? mk3(M.a[0], M.a[1], M.a[2]) : splat3(0);
+}
+BDPT_HD f3 bsdf_f_pt(const DMat& M, f3 wo, f3 wi) {   // BSDF::f of every kind (bsdf.cpp, advanced_bsdf.cpp)
+  if (M.type == MAT_DIFFUSE) {
+    if (wo.z < 0 || wi.z < 0) return splat3(0);
+    return divs(mk3(M.a[0], M.a[1], M.a[2]), BDPT_PI_F);
+  }
+  if (M.type == MAT_MICROFACET) return mf_f(M, wo, wi);
+  return splat3(0);
+}
+// SceneLight::sample_L (light.cpp:103-113, 205-217; environment_light.cpp:126-156)
+BDPT_HD f3 light_sample_L(const SceneView& S, const DLight& L, Rng& g, f3 p, f3* wi, float* dist, float* pdf) {
+  if (L.type == LIGHT_ENV) {
+    *dist = INFINITY;
+    return env_sample_dir(S.env, g, wi, pdf);
+  }
+  if (L.type == LIGHT_POINT) {
+    const f3 d = sub(mk3(L.pos[0], L.pos[1], L.pos[2]), p);
+    *wi = normalize(d);
+    *dist = norm(d);
+    *pdf = 1.0f;
+    return mk3(L.rad[0], L.rad[1], L.rad[2]);
+  }
+  float sx, sy;
+  grid2d(g, &sx, &sy);
+  sx = sx - 0.5f;
+  sy = sy - 0.5f;
+  const f3 d = sub(add(add(mk3(L.pos[0], L.pos[1], L.pos[2]), smul(sx, mk3(L.dx[0], L.dx[1], L.dx[2]))),
+                       smul(sy, mk3(L.dy[0], L.dy[1], L.dy[2]))), p);
+  const float cosT = dot(d, mk3(L.dir[0], L.dir[1], L.dir[2]));
+  const float sq = norm2(d);
+  const float dd = sqrtf(sq);
+  *wi = divs(d, dd);
+  *dist = dd;
+  *pdf = sq / (L.area * fabsf(cosT));
+  return cosT < 0 ? mk3(L.rad[0], L.rad[1], L.rad[2]) : splat3(0);
+}
+
+// Direct lighting at a non-delta hit (estimate_direct_lighting_importance :99-169 /
+// _hemisphere :47-97).
+template <int LM>
+BDPT_HD f3 pt_direct(const SceneView& S, const PtParams& pp, Rng& g, const Frame& fr, f3 hit_p, f3 w_out, f3 n,
+                     const DMat& M, Counters& cnt) {
+  f3 L_out = splat3(0);
+  if (pp.hemisphere) {
+    const int num = S.nlights * pp.ns_area_light;
+    for (int i = 0; i < num; i++) {
+      f3 wi;
+      float pdf;
+      const f3 f = sample_f(M, g, w_out, &wi, &pdf);
+      const f3 wiw = normalize(to_world(fr, wi));
+      Hit h;
+      if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h, cnt)) continue;
+      f3 hn;
+      int hm;
+      shade_hit(S, h, hit_p, wiw, &hn, &hm);
+      const float ct = fabsf(dot(wiw, n));
+      L_out = add(L_out, divs(muls(mul(mat_emission(S, hm), f), ct), pdf));
+    }
+    return divs(L_out, (float)num);
+  }
+  for (int l = 0; l < S.nlights; l++) {
+    const DLight& L = S.lights[l];
+    const int ns = L.type == LIGHT_POINT ? 1 : pp.ns_area_light;
+    f3 L_o = splat3(0);
+    for (int i = 0; i < ns; i++) {
+      f3 wiw;
+      float dist, pdf;
+      const f3 Le = light_sample_L(S, L, g, hit_p, &wiw, &dist, &pdf);
+      const f3 f = bsdf_f_pt(M, w_out, to_local(fr, wiw));
+      if (trace_any<LM, BDPT_CONN_STACK>(S, hit_p, wiw, BDPT_EPS_F, dist - BDPT_EPS_F, cnt)) continue;
+      const float ct = fabsf(dot(wiw, n));
+      const f3 L_in = dist >= INFINITY ? Le : divs(Le, dist * dist);
+      L_o = add(L_o, divs(muls(mul(L_in, f), ct), pdf));
+    }
+    L_out = add(L_out, divs(L_o, (float)ns));
+  }
+  return L_out;
+}
+
+// One camera sample (raytrace_pixel :304-316 -> est_radiance_global_illumination :264-290).
+template <int LM>
+BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int x, int y, uint32_t sample) {
+  Rng g;
+  rng_init(g, pp.seed, (uint32_t)(x + y * pp.W), sample);
+  float px, py, lx, ly;
+  grid2d(g, &px, &py);
+  px = px + (float)x;
+  py = py + (float)y;
+  const float dx = px / (float)pp.W, dy = py / (float)pp.H;
+  grid2d(g, &lx, &ly);
+  // Camera::generate_ray_for_thin_lens (camera_lens.cpp:22-43)
+  float lc, ls;
+  cos_sin_2pi(ly, &lc, &ls);
+  const f3 pLens = mk3(pp.lens_radius * sqrtf(lx) * lc, pp.lens_radius * sqrtf(lx) * ls, 0.0f);
+  const f3 rdir = mk3((2 * dx - 1) * S.cam.tanh_, (2 * dy - 1) * S.cam.tanv_, -1.0f);
+  const f3 rd0 = sub(muls(rdir, pp.focal_distance), pLens);
+  const f3 c0 = mk3(S.cam.c2w[0], S.cam.c2w[1], S.cam.c2w[2]), c1 = mk3(S.cam.c2w[3], S.cam.c2w[4], S.cam.c2w[5]),
+           c2 = mk3(S.cam.c2w[6], S.cam.c2w[7], S.cam.c2w[8]);
+  f3 rd = normalize(add(add(smul(rd0.x, c0), smul(rd0.y, c1)), smul(rd0.z, c2)));
+  f3 ro = add(mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]),
+              add(add(smul(pLens.x, c0), smul(pLens.y, c1)), smul(pLens.z, c2)));
+  Hit h;
+  if (!trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, S.cam.nclip, S.cam.fclip, h, cnt))
+    return S.env.light >= 0 ? env_radiance(S.env, rd) : splat3(0);
+  f3 n;
+  int mat;
+  shade_hit(S, h, ro, rd, &n, &mat);
+  const f3 E0 = mat_emission(S, mat);
+  // forward walk: per vertex k the NEE value, and for a continued walk f, cos, pdf, the roulette
+  // flag and the next hit's emission (used when vertex k is delta)
+  f3 nee[kPtMaxVerts], fk[kPtMaxVerts], enext[kPtMaxVerts];
+  float ck[kPtMaxVerts], pk[kPtMaxVerts];
+  unsigned delta_m = 0, cont_m = 0;
+  const bool roulette = pp.max_depth == 0;
+  int k = 0;
+  for (;; k++) {
+    const DMat M = S.mats[mat];
+    const Frame fr = make_frame(n);
+    const f3 hit_p = add(ro, muls(rd, h.t));
+    const f3 w_out = to_local(fr, neg(rd));
+    const bool dl = is_delta(M.type);
+    if (dl) delta_m |= 1u << k;
+    nee[k] = dl ? splat3(0) : pt_direct<LM>(S, pp, g, fr, hit_p, w_out, n, M, cnt);
+    bool trace;
+    if (roulette) trace = (rng_next(g) < 0.3f) && k < 20;
+    else trace = k < pp.max_depth - 1;
+    if (!trace || k + 1 >= kPtMaxVerts) break;
+    f3 wi;
+    float pdf;
+    const f3 f = sample_f(M, g, w_out, &wi, &pdf);
+    const f3 wiw = normalize(to_world(fr, wi));
+    Hit h2;
+    if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h2, cnt)) break;
+    f3 n2;
+    int m2;
+    shade_hit(S, h2, hit_p, wiw, &n2, &m2);
+    fk[k] = f;
+    ck[k] = fabsf(dot(wiw, n));
+    pk[k] = pdf;
+    enext[k] = mat_emission(S, m2);
+    cont_m |= 1u << k;
+    ro = hit_p; rd = wiw; h = h2; n = n2; mat = m2;
+  }
+  // fold innermost-first: L_k = nee_k + (L_{k+1} [+ E_{k+1} if delta_k]) * f_k * cos_k / pdf_k [/ 0.3]
+  f3 L = splat3(0);
+  for (int j = k; j >= 0; j--) {
+    f3 Lj = add(splat3(0), nee[j]);
+    if ((cont_m >> j) & 1u) {
+      f3 L_in = L;
+      if ((delta_m >> j) & 1u) L_in = add(L_in, enext[j]);
+      f3 t = divs(muls(mul(L_in, fk[j]), ck[j]), pk[j]);
+      if (roulette) t = divs(t, 0.3f);
+      Lj = add(Lj, add(splat3(0), t));
+    }
+    L = Lj;
+  }
+  return add(E0, L);
+}
+
+// PathTracer::raytrace_pixel's adaptive batches (:292-338): samples in batches of pp.batch until
+// the 95% interval of the illuminance is within tol * mean (or pp.spp is reached).
+template <int LM>
+BDPT_HD f3 pt_pixel(const SceneView& S, const PtParams& pp, Counters& cnt, int x, int y, int* count) {
+  int num = 0;
+  f3 illum = splat3(0);
+  float s1 = 0, s2 = 0;
+  for (int i = 0; i < pp.spp; i += pp.batch) {
+    for (int j = 0; j < pp.batch; j++) {
+      const f3 ill = pt_sample<LM>(S, pp, cnt, x, y, (uint32_t)(i + j));
+      illum = add(illum, ill);
+      const float il = 0.2126f * ill.x + 0.7152f * ill.y + 0.0722f * ill.z;   // Vector3D::illum
+      s1 += il;
+      s2 += il * il;
+    }
+    num = i + pp.batch;
+    const float mu = s1 / (float)num;
+    const float sigma = sqrtf((s2 - s1 * s1 / (float)num) / (float)(num - 1));
+    const float ci = 1.96f * sigma / sqrtf((float)num);
+    if (ci <= pp.tol * mu && mu > BDPT_EPS_F) break;
+  }
+  *count = num;
+  return divs(illum, (float)num);
 }
 
 }  // namespace bdpt

@@ -36,6 +36,8 @@ struct Ctx {
   DLight* d_lights = nullptr;
   int* d_prim_ref = nullptr;
   float* d_env = nullptr;      // HostScene::env (environment light tables + map)
+  int* d_count = nullptr;      // PathTracer::sampleCountBuffer (W*H)
+  bool pt = false;             // bdpt_params.integrator == BDPT_INTEGRATOR_PT
   float* d_eye = nullptr;
   float* d_light = nullptr;
   float* d_sample = nullptr;

@@ -421,6 +421,74 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   }
 }
 
+// k_pt: the unidirectional PathTracer (bdpt_core.h pt_pixel). Persistent waves take 8x8 pixel
+// blocks from a ticket counter; a lane owns one pixel and runs its adaptive batches to the end
+// (PathTracer::raytrace_pixel), then stores the mean (update_pixel) and the sample count.
+struct PtKParams {
+  SceneView S;
+  PtParams pp;
+  float* eye;                 // the frame (sampleBuffer)
+  int* count;                 // sampleCountBuffer
+  unsigned long long* stats;
+  const int4* blocks;
+  int nblocks, nbx;
+  unsigned* work;
+  int n_node4, n_geom4;
+};
+
+template <bool STATS, int LM>
+__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_pt(PtKParams kp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  if (LM != 0) {
+    float4* sc = (float4*)smem;
+    const int nn = LM == 1 ? kp.n_node4 : node_f4(lm_width(LM)) * kp.S.ntop;
+    const int n4 = nn + (LM == 1 ? kp.n_geom4 : 0);
+    for (int k = threadIdx.x; k < n4; k += blockDim.x) sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
+    __syncthreads();
+    kp.S.lnodes = sc;
+    kp.S.lgeom = sc + nn;
+  }
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  unsigned nsamp = 0;
+  for (;;) {
+    unsigned item = 0;
+    if (lane == 0) item = atomicAdd(kp.work, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= (unsigned)kp.nblocks) break;
+    int bx0, by0, bw, bh;
+    if (kp.blocks) {
+      const int4 bb = kp.blocks[item];
+      bx0 = bb.x; by0 = bb.y; bw = bb.z; bh = bb.w;
+    } else {
+      bx0 = ((int)item % kp.nbx) * 8;
+      by0 = ((int)item / kp.nbx) * 8;
+      bw = min(8, kp.pp.W - bx0);
+      bh = min(8, kp.pp.H - by0);
+    }
+    const int qx = lane & 7, qy = lane >> 3;
+    if (qx < bw && qy < bh) {
+      const int x = bx0 + qx, y = by0 + qy;
+      int n = 0;
+      const f3 v = pt_pixel<LM>(kp.S, kp.pp, cnt, x, y, &n);
+      const size_t k = (size_t)x + (size_t)y * kp.pp.W;
+      kp.eye[3 * k] = v.x;
+      kp.eye[3 * k + 1] = v.y;
+      kp.eye[3 * k + 2] = v.z;
+      kp.count[k] = n;
+      nsamp += (unsigned)n;
+    }
+  }
+  if (STATS) {
+    unsigned v[7] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      unsigned s = wave_sum(v[k]);
+      if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
+    }
+  }
+}
+
 __global__ void k_trace_rays(SceneView S, const float* rays, int n, int any_hit, float* out_t, int* out_prim,
                              const int* prim_ref) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -488,9 +556,36 @@ int launch_maxv(Ctx* c, KParams& kp) {
   return c->prm.collect_stats ? launch_lm<MAXV, true, false>(c, kp) : launch_lm<MAXV, false, false>(c, kp);
 }
 
+template <class K, class KP>
+int launch_persistent_pt(Ctx* c, K kernel, size_t lds, const KP& kp, long long items) {
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BDPT_BLOCK, lds));
+  if (per_cu <= 0) { g_err = "k_pt cannot be resident (LDS/VGPR budget)"; return BDPT_E_DEVICE; }
+  long long grid = std::min<long long>((long long)per_cu * c->ncu, (items + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)std::max(1LL, grid)), dim3(BDPT_BLOCK), lds, c->stream, kp);
+  HIPCHK(hipGetLastError());
+  return BDPT_OK;
+}
+
+template <bool STATS>
+int launch_pt(Ctx* c, PtKParams& kp) {
+  const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
+  const size_t lds_max = kLdsPerCu / kBlocksPerCu - 256;
+  const char* env = getenv("BDPT_LDS_MODE");
+  int lm = env ? atoi(env) : (full <= lds_max ? 1 : 2);
+  if (lm == 1 && full > lds_max) lm = 2;
+  kp.S = view_of(c, lm);
+  kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
+  kp.n_geom4 = (int)(c->hs.geom.size() / 4);
+  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, lds_max / node_bytes(lm_width(2)));
+  if (lm == 1) return launch_persistent_pt(c, k_pt<STATS, 1>, full, kp, kp.nblocks);
+  if (lm == 2) return launch_persistent_pt(c, k_pt<STATS, 2>, (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp, kp.nblocks);
+  return launch_persistent_pt(c, k_pt<STATS, 0>, 0, kp, kp.nblocks);
+}
+
 void free_ctx(Ctx* c) {
   if (!c) return;
-  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env,
+  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count,
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -535,10 +630,15 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   int pipe = p.pipeline;
   if (const char* pe = getenv("BDPT_PIPELINE")) pipe = atoi(pe);
   c->pipeline = pipe == 2 ? PIPE_WAVEFRONT : PIPE_MEGAKERNEL;
-  int rc = build_host_scene(scene, c->hs, g_err);
+  c->pt = p.integrator == BDPT_INTEGRATOR_PT;
+  if (p.integrator != BDPT_INTEGRATOR_BDPT && !c->pt) { g_err = "unknown integrator"; delete c; return BDPT_E_INVALID; }
+  if (c->pt && (p.ns_area_light < 0 || p.samples_per_batch < 0 || p.lens_radius < 0)) {
+    g_err = "invalid PathTracer settings"; delete c; return BDPT_E_INVALID;
+  }
+  int rc = build_host_scene(scene, c->hs, g_err, c->pt);
   if (rc) { delete c; return rc; }
   c->ext = c->hs.env_light >= 0 || p.russian_roulette != 0;
-  if (c->ext && c->pipeline == PIPE_WAVEFRONT) {
+  if (c->ext && !c->pt && c->pipeline == PIPE_WAVEFRONT) {
     g_err = "the wavefront pipeline does not implement the environment light / Russian roulette; use pipeline 0 or 1";
     delete c;
     return BDPT_E_UNSUPPORTED;
@@ -567,6 +667,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   size_t fb = c->npix * 3 * sizeof(float);
   if (hipMalloc((void**)&c->d_eye, fb) != hipSuccess || hipMalloc((void**)&c->d_light, fb) != hipSuccess ||
       hipMalloc((void**)&c->d_sample, fb) != hipSuccess ||
+      hipMalloc((void**)&c->d_count, c->npix * sizeof(int)) != hipSuccess ||
       hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "out of device memory";
     return fail(BDPT_E_NOMEM);
@@ -579,6 +680,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->stream = c->own;
   if (hipMemsetAsync(c->d_eye, 0, fb, c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_light, 0, fb, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_count, 0, c->npix * sizeof(int), c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess) { g_err = "init sync failed"; return fail(BDPT_E_DEVICE); }
   *ctx_out = c;
@@ -607,6 +709,7 @@ int bdpt_clear(void* ctx) {
   size_t fb = c->npix * 3 * sizeof(float);
   HIPCHK(hipMemsetAsync(c->d_eye, 0, fb, c->stream));
   HIPCHK(hipMemsetAsync(c->d_light, 0, fb, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_count, 0, c->npix * sizeof(int), c->stream));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream));
   return BDPT_OK;
 }
@@ -654,6 +757,35 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
     HIPCHK(hipMemcpyAsync(c->d_blocks, c->h_blocks, blk.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
     kp.blocks = c->d_blocks;
     kp.nblocks = (int)blk.size();
+  }
+  if (c->pt) {   // the PathTracer renders whole pixels (adaptive sampling decides per pixel)
+    if (spp_begin != 0 || spp_count != c->prm.spp) {
+      g_err = "the PathTracer renders whole pixels: spp_begin must be 0 and spp_count the ctx's spp";
+      return BDPT_E_INVALID;
+    }
+    PtKParams pk;
+    pk.pp.W = W; pk.pp.H = H; pk.pp.spp = c->prm.spp; pk.pp.max_depth = c->prm.max_depth;
+    pk.pp.seed = c->prm.seed;
+    pk.pp.ns_area_light = c->prm.ns_area_light > 0 ? c->prm.ns_area_light : 1;
+    pk.pp.batch = c->prm.samples_per_batch > 0 ? c->prm.samples_per_batch : 32;
+    pk.pp.hemisphere = c->prm.direct_hemisphere_sample != 0;
+    pk.pp.tol = c->prm.max_tolerance;
+    pk.pp.lens_radius = (float)c->prm.lens_radius;
+    pk.pp.focal_distance = (float)(c->prm.focal_distance > 0 ? c->prm.focal_distance : 4.7);
+    pk.eye = c->d_eye;
+    pk.count = c->d_count;
+    pk.stats = c->d_stats;
+    pk.blocks = kp.blocks;
+    pk.nblocks = kp.nblocks;
+    pk.nbx = kp.nbx;
+    pk.work = (unsigned*)(c->d_stats + 15);
+    HIPCHK(hipMemsetAsync(pk.work, 0, sizeof(unsigned), c->stream));
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    int rc = c->prm.collect_stats ? launch_pt<true>(c, pk) : launch_pt<false>(c, pk);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return BDPT_OK;
   }
   if (c->pipeline == PIPE_WAVEFRONT) {
     HIPCHK(hipEventRecord(c->ev0, c->stream));
@@ -728,6 +860,19 @@ int bdpt_read_frame(void* ctx, int32_t which, float* rgb) {
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(rgb, p, c->npix * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return BDPT_OK;
+}
+
+int bdpt_read_sample_counts(void* ctx, int32_t* counts) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !counts) { g_err = "null argument"; return BDPT_E_INVALID; }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->pt) {
+    HIPCHK(hipMemcpy(counts, c->d_count, c->npix * sizeof(int), hipMemcpyDeviceToHost));
+  } else {   // BidirectionalPathTracer::raytrace_pixel records ns_aa (bidirection.cpp:539)
+    for (size_t k = 0; k < c->npix; k++) counts[k] = c->prm.spp;
+  }
   return BDPT_OK;
 }
 

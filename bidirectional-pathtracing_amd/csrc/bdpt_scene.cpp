@@ -218,7 +218,7 @@ float i2f(int v) {
 
 }  // namespace
 
-int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err) {
+int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err, bool pt) {
   if (!d || d->nprim <= 0 || !d->prim_type || !d->prim_geom || !d->prim_mat) {
     err = "scene has no primitives";
     return BDPT_E_INVALID;
@@ -230,15 +230,16 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err)
   out.mats.clear();
   for (int i = 0; i < d->nmat; i++) {
     const bdpt_material& m = d->mats[i];
-    if (m.type == BDPT_MAT_MICROFACET) {
+    if (m.type == BDPT_MAT_MICROFACET && !pt) {
       err = "MicrofacetBSDF::sample_pdf is assert(0) under BDPT (advanced_bsdf.cpp:144-148)";
       return BDPT_E_UNSUPPORTED;
     }
-    if (m.type < BDPT_MAT_DIFFUSE || m.type > BDPT_MAT_REFRACTION) { err = "unknown material type"; return BDPT_E_INVALID; }
+    if (m.type < BDPT_MAT_DIFFUSE || m.type > BDPT_MAT_MICROFACET) { err = "unknown material type"; return BDPT_E_INVALID; }
     DMat M;
     M.type = m.type;
     for (int k = 0; k < 3; k++) { M.a[k] = (float)m.a[k]; M.b[k] = (float)m.b[k]; }
     M.ior = (float)m.ior;
+    M.alpha = (float)m.roughness;
     out.mats.push_back(M);
   }
   // lights (light.cpp:102-284)

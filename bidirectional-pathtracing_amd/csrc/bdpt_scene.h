@@ -55,6 +55,7 @@ struct HostScene {
 constexpr int kTopNodes = 1024;
 
 // Returns BDPT_OK or an error code; err receives a message.
-int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err);
+// pt: the scene is for the unidirectional PathTracer (microfacet materials allowed).
+int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err, bool pt = false);
 
 }  // namespace bdpt

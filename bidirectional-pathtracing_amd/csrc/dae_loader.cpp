@@ -541,9 +541,12 @@ struct Parser {
           mat = Material();
           mat.type = BDPT_MAT_MIRROR;
           mat.a = spectrum_of(txt("reflectance"));
-        } else if (ty == "microfacet") {
+        } else if (ty == "microfacet") {   // collada.cpp:886-895: a = eta, b = k, alpha as float
           mat = Material();
           mat.type = BDPT_MAT_MICROFACET;
+          mat.a = spectrum_of(txt("eta"));
+          mat.b = spectrum_of(txt("k"));
+          mat.roughness = (float)atof(txt("alpha") ? txt("alpha") : "0");
         } else if (ty == "refraction") {
           mat = Material();
           mat.type = BDPT_MAT_REFRACTION;
@@ -981,7 +984,11 @@ int dump_scene_json(const DaeScene& s, const char* path, std::string& err) {
         fprintf(f, "{\"type\": \"refraction\", \"transmittance\": "); v3(m.b);
         fprintf(f, ", \"roughness\": %.17g, \"ior\": %.17g}", m.roughness, m.ior);
         break;
-      default: fprintf(f, "{\"type\": \"microfacet\"}"); break;
+      default:
+        fprintf(f, "{\"type\": \"microfacet\", \"eta\": "); v3(m.a);
+        fprintf(f, ", \"k\": "); v3(m.b);
+        fprintf(f, ", \"alpha\": %.17g}", m.roughness);
+        break;
     }
   }
   fprintf(f, "],\n\"prim_order\": [");

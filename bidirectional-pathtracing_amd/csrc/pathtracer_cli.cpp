@@ -2,13 +2,16 @@
 // in windowless mode, rendering through libbdpt_amd.so on MI355X GPUs.
 //
 //   pathtracer [-s spp] [-m max_depth] [-r W H] [-f out.png] [-p x y dx dy] [-t threads]
-//              [-l n] [-e envmap.exr] [--rr] [-g gpus] [-S seed] [--dump-scene scene.json] scene.dae
+//              [-l n] [-e envmap.exr] [--rr] [-g gpus] [-S seed] [--dump-scene scene.json]
+//              [--pt [-a batch tol] [-H] [-b lens] [-d focal]] scene.dae
 //
 // Same flags and defaults as the reference (-s 1, -m 1, 800x600 when -r is absent; -t / -l are
 // accepted and do not apply to the GPU path; -p renders one cell). -g N splits the sample range
 // over N devices (one context and one host thread per device) and sums the frames. -e loads an
 // environment map as the reference's -e does (load_exr, main.cpp:115-119) — under BDPT, which the
 // reference cannot run with it; --rr turns on Russian roulette (bidirection.cpp:87-93).
+// --pt selects the reference's unidirectional PathTracer (pathtracer.cpp:47-340) with its flags
+// -l, -a, -H, -b, -d (main.cpp:107-141); its -g N splits the frame into row bands (whole pixels).
 // Output: the tonemapped PNG and the "_rate.png" sampling-rate image, as render_to_file writes
 // them (raytraced_renderer.cpp:330-347, 690-761).
 #include <chrono>
@@ -31,6 +34,11 @@ void usage(const char* b) {
   printf("  -l  <INT>        Number of samples per area light (unused by BDPT)\n");
   printf("  -t  <INT>        Number of render threads (GPU path: ignored)\n");
   printf("  -m  <INT>        Maximum ray depth\n");
+  printf("  --pt             Unidirectional PathTracer instead of BDPT\n");
+  printf("  -a  <INT> <FLOAT> PathTracer: samples per batch and tolerance (adaptive sampling)\n");
+  printf("  -H               PathTracer: hemisphere sampling for direct lighting\n");
+  printf("  -b  <FLOAT>      PathTracer: lens radius\n");
+  printf("  -d  <FLOAT>      PathTracer: focal distance\n");
   printf("  -e  <PATH>       Path to environment map\n");
   printf("  --rr             Russian roulette on both subpaths\n");
   printf("  -f  <FILENAME>   Image (.png) file to save output to\n");
@@ -56,7 +64,10 @@ int main(int argc, char** argv) {
   long cx = -1, cy = 0, cdx = 0, cdy = 0;
   unsigned long long seed = 5489;
   std::string out, dump, scene, envpath;
-  bool rr = false;
+  bool rr = false, pt = false, hemi = false;
+  int nal = 1, batch = 32;
+  float tol = 0.05f;
+  double lens = 0.0, focal = 4.7;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto need = [&](int n) {
@@ -64,7 +75,13 @@ int main(int argc, char** argv) {
     };
     if (a == "-s") { need(1); spp = atoi(argv[++i]); }
     else if (a == "-m") { need(1); max_depth = atoi(argv[++i]); }
-    else if (a == "-t" || a == "-l") { need(1); ++i; }
+    else if (a == "-t") { need(1); ++i; }
+    else if (a == "-l") { need(1); nal = atoi(argv[++i]); }
+    else if (a == "--pt") pt = true;
+    else if (a == "-a") { need(2); batch = atoi(argv[i + 1]); tol = (float)atof(argv[i + 2]); i += 2; }
+    else if (a == "-H") hemi = true;
+    else if (a == "-b") { need(1); lens = atof(argv[++i]); }
+    else if (a == "-d") { need(1); focal = atof(argv[++i]); }
     else if (a == "-f") { need(1); out = argv[++i]; }
     else if (a == "-r") { need(2); w = atoi(argv[i + 1]); h = atoi(argv[i + 2]); i += 2; }
     else if (a == "-p") { need(4); cx = atol(argv[i + 1]); cy = atol(argv[i + 2]); cdx = atol(argv[i + 3]); cdy = atol(argv[i + 4]); i += 4; }
@@ -87,7 +104,7 @@ int main(int argc, char** argv) {
       if (!bdpt::write_png(o, bdpt::tonemap(hdr.data(), tw, tht), tw, tht)) return 1;
       return bdpt::write_rate_png(o, std::vector<float>((size_t)tw * tht, 1.0f), tw, tht) ? 0 : 1;
     }
-    else if (a == "-c" || a == "-b" || a == "-d") {
+    else if (a == "-c") {
       fprintf(stderr, "[PathTracer] option %s is not supported by the BDPT GPU path\n", a.c_str());
       return 1;
     } else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
@@ -121,6 +138,7 @@ int main(int argc, char** argv) {
   if (cx >= 0) tiles.push_back(bdpt_tile{(int32_t)cx, (int32_t)cy, (int32_t)cdx, (int32_t)cdy});
   std::vector<std::vector<float>> frames(gpus, std::vector<float>((size_t)w * h * 3, 0.0f));
   std::vector<int> rcs(gpus, 0);
+  std::vector<std::vector<int32_t>> counts(gpus, std::vector<int32_t>((size_t)w * h, 0));
   std::vector<std::string> errs(gpus);
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
@@ -130,12 +148,25 @@ int main(int argc, char** argv) {
       memset(&p, 0, sizeof p);
       p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed; p.device = g;
       p.russian_roulette = rr ? 1 : 0;
+      if (pt) {
+        p.integrator = BDPT_INTEGRATOR_PT;
+        p.ns_area_light = nal; p.samples_per_batch = batch; p.max_tolerance = tol;
+        p.direct_hemisphere_sample = hemi ? 1 : 0; p.lens_radius = lens; p.focal_distance = focal;
+      }
       void* ctx = nullptr;
-      const int s0 = (int)((long long)spp * g / gpus), s1 = (int)((long long)spp * (g + 1) / gpus);
+      int s0 = (int)((long long)spp * g / gpus), s1 = (int)((long long)spp * (g + 1) / gpus);
+      std::vector<bdpt_tile> mine = tiles;
+      if (pt) {   // whole pixels: GPU g takes a band of rows (or of the -p cell)
+        bdpt_tile area = tiles.empty() ? bdpt_tile{0, 0, (int32_t)w, (int32_t)h} : tiles[0];
+        const int r0 = area.y0 + (int)((long long)area.h * g / gpus), r1 = area.y0 + (int)((long long)area.h * (g + 1) / gpus);
+        mine.assign(1, bdpt_tile{area.x0, r0, area.w, r1 - r0});
+        s0 = 0; s1 = r1 > r0 ? spp : 0;
+      }
       int rc = bdpt_create(&desc, &p, &ctx);
       if (rc == BDPT_OK && s1 > s0)
-        rc = bdpt_render(ctx, tiles.empty() ? nullptr : tiles.data(), (int32_t)tiles.size(), s0, s1 - s0);
+        rc = bdpt_render(ctx, mine.empty() ? nullptr : mine.data(), (int32_t)mine.size(), s0, s1 - s0);
       if (rc == BDPT_OK) rc = bdpt_read_frame(ctx, BDPT_FRAME_SAMPLE, frames[g].data());
+      if (rc == BDPT_OK) rc = bdpt_read_sample_counts(ctx, counts[g].data());
       if (rc != BDPT_OK) errs[g] = bdpt_last_error();
       if (ctx) bdpt_destroy(ctx);
       rcs[g] = rc;
@@ -161,7 +192,13 @@ int main(int argc, char** argv) {
   if (!bdpt::write_png(out, rgba, w, h)) { fprintf(stderr, "failed\n"); return 1; }
   fprintf(stderr, "Done!\n");
   std::vector<float> rate((size_t)w * h, 0.0f);
-  if (tiles.empty()) {
+  if (pt) {   // sampleCountBuffer[k] * 1.0f / ns_aa (save_sampling_rate_image, raytraced_renderer.cpp:737)
+    for (size_t k = 0; k < rate.size(); k++) {
+      int32_t n = 0;
+      for (int g = 0; g < gpus; g++) n += counts[g][k];
+      rate[k] = n * 1.0f / spp;
+    }
+  } else if (tiles.empty()) {
     std::fill(rate.begin(), rate.end(), 1.0f);   // every pixel got ns_aa samples (bidirection.cpp:539)
   } else {
     for (long y = std::max(0L, cy); y < std::min((long)h, cy + cdy); y++)

@@ -26,6 +26,9 @@
  *     environment_light.cpp:182-208): bdpt_scene_desc.envmap, loaded by bdpt_exr_load (-e);
  *   - Russian roulette on both subpaths through PathVertex.q (bidirection.h:36, the rule commented
  *     out at bidirection.cpp:87-93): bdpt_params.russian_roulette.
+ * And the reference's second integrator: the unidirectional PathTracer
+ * (pathtracer.cpp:47-340 — NEE, adaptive sampling, thin lens, roulette at -m 0, the environment
+ * light, MicrofacetBSDF), selected by bdpt_params.integrator = BDPT_INTEGRATOR_PT (ABI v3).
  */
 #ifndef BDPT_AMD_BDPT_H
 #define BDPT_AMD_BDPT_H
@@ -37,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 2
+#define BDPT_ABI_VERSION 3
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -130,8 +133,19 @@ typedef struct bdpt_params {
   int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
   int32_t pipeline;           /* 0 = auto, 1 = megakernel, 2 = wavefront; same results     */
   int32_t russian_roulette;   /* 1 = PathVertex.q roulette on both subpaths (ABI v2)       */
-  int32_t reserved[3];
+  /* ABI v3: the integrator and the PathTracer's settings (PathTracer fields, pathtracer.h:73-85;
+   * CLI -l -a -H -b -d, main.cpp:107-141; AppConfig defaults application.h:45-65) */
+  int32_t integrator;         /* BDPT_INTEGRATOR_BDPT (0, the reference's) / _PT (1)         */
+  int32_t ns_area_light;      /* -l: samples per area light (0 = 1)                          */
+  int32_t samples_per_batch;  /* -a batch: adaptive sampling batch (0 = 32)                  */
+  float max_tolerance;        /* -a tol: stop when 1.96 sigma / sqrt(n) <= tol * mean        */
+  int32_t direct_hemisphere_sample;  /* -H: hemisphere instead of light sampling            */
+  double lens_radius;         /* -b (0: pinhole)                                             */
+  double focal_distance;      /* -d (0 = 4.7)                                                */
+  int32_t reserved[4];
 } bdpt_params;
+
+enum bdpt_integrator { BDPT_INTEGRATOR_BDPT = 0, BDPT_INTEGRATOR_PT = 1 };
 
 typedef struct bdpt_tile {
   int32_t x0, y0, w, h;       /* clipped to the frame like raytrace_tile does            */
@@ -168,14 +182,21 @@ int bdpt_set_stream(void* ctx, void* stream);
 int bdpt_clear(void* ctx);
 
 /* Renders global sample indices [spp_begin, spp_begin+spp_count) of every pixel of the tiles.
- * Asynchronous on the ctx stream. ntiles == 0 or tiles == NULL means the whole frame. */
+ * Asynchronous on the ctx stream. ntiles == 0 or tiles == NULL means the whole frame. The
+ * PathTracer renders whole pixels (its adaptive sampling decides per pixel): spp_begin must be 0
+ * and spp_count the ctx's spp; shard its work across GPUs by tiles. */
 int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_begin,
                 int32_t spp_count);
 
 int bdpt_sync(void* ctx);
 
-/* Copies a W*H*3 float frame (row 0 = bottom, as HDRImageBuffer) to host memory (sync). */
+/* Copies a W*H*3 float frame (row 0 = bottom, as HDRImageBuffer) to host memory (sync). Under
+ * the PathTracer, BDPT_FRAME_SAMPLE is its sampleBuffer (per-pixel means, update_pixel). */
 int bdpt_read_frame(void* ctx, int32_t which, float* rgb);
+
+/* PathTracer::sampleCountBuffer (pathtracer.h:94): W*H samples per pixel, row 0 = bottom (sync).
+ * Under BDPT every rendered pixel reports the samples rendered for it. */
+int bdpt_read_sample_counts(void* ctx, int32_t* counts);
 
 /* Device pointer of a frame (W*H*3 float) for in-HBM consumers (RCCL reduce). */
 int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr);

@@ -149,10 +149,14 @@ struct CounterStream {
 struct RefStreams {
   std::mt19937 S;   // sampler.cpp's engine (all Sampler2D/3D draws)
   std::mt19937 G;   // advanced_bsdf.cpp's engine (GlassBSDF coin_flip)
+  std::mt19937 P;   // pathtracer.cpp's engine (PathTracer's roulette coin_flip)
+  std::mt19937 E;   // environment_light.cpp's engine (sample_L's texel jitter)
   double rmax = 1.0 / (double)(4294967295u);
   static double clampd(double x) { return std::min(std::max(x, 0.0000001), 0.99999999); }
   double uS() { return clampd(double(S()) * rmax); }
   double uG() { return clampd(double(G()) * rmax); }
+  double uP() { return clampd(double(P()) * rmax); }
+  double uE() { return clampd(double(E()) * rmax); }
 };
 
 // ----------------------------------------------------------------------------------------------
@@ -163,6 +167,8 @@ struct PolicyRef {              // mode 0
   RefStreams* rs;
   R uS() { return rs->uS(); }
   R uG() { return rs->uG(); }
+  R uP() { return rs->uP(); }
+  R uE() { return rs->uE(); }
   int rand_light(int n) { return 0 + std::rand() % (n - 1 - 0 + 1); }   // sampler.h:25-28
   void stream(uint32_t) {}                                                  // one sequential stream
   static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
@@ -179,6 +185,8 @@ struct PolicyC64 {              // mode 1
   CounterStream* cs;
   R uS() { return (double)cs->next(); }
   R uG() { return (double)cs->next(); }
+  R uP() { return (double)cs->next(); }
+  R uE() { return (double)cs->next(); }
   int rand_light(int n) { int k = (int)((double)cs->next() * n); return k < n ? k : n - 1; }
   void stream(uint32_t k) { cs->select(k); }
   static void cos_sin_2pi(R xi, R* c, R* s) { R th = 2. * PI_D * xi; *c = std::cos(th); *s = std::sin(th); }
@@ -246,6 +254,8 @@ struct PolicyC32 {              // mode 2
   CounterStream* cs;
   R uS() { return cs->next(); }
   R uG() { return cs->next(); }
+  R uP() { return cs->next(); }
+  R uE() { return cs->next(); }
   int rand_light(int n) { int k = (int)(cs->next() * (float)n); return k < n ? k : n - 1; }
   void stream(uint32_t k) { cs->select(k); }
   static void cos_sin_2pi(R xi, R* c, R* s) { cos_sin_2pi_f32(xi, c, s); }
@@ -294,8 +304,9 @@ struct Prim {
 template <class R>
 struct Mat {
   int type;
-  V3<R> a, b;
+  V3<R> a, b;          // microfacet: a = eta, b = k (MicrofacetBSDF, bsdf.h:170-205)
   R ior;
+  R alpha = 0;         // microfacet roughness (collada.cpp:891, parsed as float)
 };
 
 template <class R>
@@ -423,7 +434,7 @@ static float pad_up(double v, double ext) {
 }
 
 template <class R>
-static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) {
+static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err, bool pt = false) {
   // Primitives (Triangle ctor triangle.cpp:9-21; Sphere sphere.h:23) in fp64, then precision R.
   std::vector<BBoxT<double>> pb(d->nprim);
   sc.prims.resize(d->nprim);
@@ -455,7 +466,7 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) 
   }
   for (int i = 0; i < d->nmat; i++) {
     const bdpt_material& m = d->mats[i];
-    if (m.type == BDPT_MAT_MICROFACET || m.type < 0 || m.type > BDPT_MAT_MICROFACET) {
+    if ((m.type == BDPT_MAT_MICROFACET && !pt) || m.type < 0 || m.type > BDPT_MAT_MICROFACET) {
       err = "unsupported material (microfacet sample_pdf asserts under BDPT)";
       return BDPT_E_UNSUPPORTED;
     }
@@ -464,6 +475,7 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err) 
     M.a = cvt<R>(v3d(m.a));
     M.b = cvt<R>(v3d(m.b));
     M.ior = (R)m.ior;
+    M.alpha = (R)m.roughness;
     sc.mats.push_back(M);
   }
   if (d->nlight < 1 && !d->envmap) { err = "scene has no light"; return BDPT_E_INVALID; }
@@ -846,12 +858,97 @@ struct Tracer {
     *wi = V(-eta * wo.x, -eta * wo.y, sgn * std::sqrt(z_sq));
     return true;
   }
+  // ---------------- MicrofacetBSDF (advanced_bsdf.cpp:46-142, bsdf.h:176-184) ----------------
+  // Modes 0/1: the reference's libm expressions; mode 2 (P::kDevEnv): the device's fp32 forms
+  // (cos(acos z) = z, tan(acos z) = sqrt(1 - z^2) / z, integer powers by products; erf / exp / log
+  // / sqrt from the fp32 math library).
+  R mf_lambda(R alpha, const V& w) const {
+    if (P::kDevEnv) {
+      const R c = std::min(std::max(w.z, R(-1.0 + 1e-5)), R(1.0 - 1e-5));
+      const R t = std::sqrt(R(1) - c * c) / c;
+      const R a = R(1) / (alpha * t);
+      return R(0.5) * (std::erf(a) - R(1) + std::exp(-a * a) / (a * R(PI_D)));
+    }
+    double theta = std::acos(std::min(std::max((double)w.z, -1.0 + 1e-5), 1.0 - 1e-5));
+    double a = 1.0 / (alpha * std::tan(theta));
+    return (R)(0.5 * (std::erf(a) - 1.0 + std::exp(-a * a) / (a * PI_D)));
+  }
+  R mf_G(R alpha, const V& wo, const V& wi) const { return R(1.0) / (R(1.0) + mf_lambda(alpha, wi) + mf_lambda(alpha, wo)); }
+  R mf_D(R alpha, const V& h) const {
+    if (P::kDevEnv) {
+      const R c = h.z;
+      const R t = std::sqrt(std::max(R(0), R(1) - c * c)) / c;
+      const R q = t / alpha;
+      const R c2 = c * c;
+      return std::exp(-(q * q)) / (R(PI_D) * alpha * alpha * (c2 * c2));
+    }
+    double theta = std::acos(h.z);
+    double nom = std::exp(-std::pow(std::tan(theta) / alpha, 2));
+    double denom = PI_D * alpha * alpha * std::pow(std::cos(theta), 4);
+    return (R)(nom / denom);
+  }
+  V mf_F(const Mat<R>& M, const V& wi) const {
+    R c = std::fabs(wi.z) / wi.norm();
+    R c2 = P::pow2(c);
+    V e2k2 = M.a * M.a + M.b * M.b;
+    V Rs = (e2k2 - R(2) * M.a * c + V(c2)) / (e2k2 + R(2) * M.a * c + V(c2));
+    V Rp = (e2k2 * c2 - R(2) * M.a * c + V(R(1))) / (e2k2 * c2 + R(2) * M.a * c + V(R(1)));
+    return (Rs + Rp) / R(2);
+  }
+  V mf_f(const Mat<R>& M, const V& wo, const V& wi) const {
+    if (wo.z <= R(EPS_F) || wi.z <= R(EPS_F)) return V();
+    V h = wo + wi;
+    h.normalize();
+    return mf_F(M, wi) * mf_G(M.alpha, wo, wi) * mf_D(M.alpha, h) / (R(4) * wo.z * wi.z);
+  }
+  V mf_sample_f(const Mat<R>& M, const V& wo, V* wi, R* pdf) {
+    R rx, ry;
+    grid2d(&rx, &ry);
+    const R alpha = M.alpha;
+    R st, ct, sp, cp, th_t;   // sin/cos theta, sin/cos phi, tan theta
+    if (P::kDevEnv) {
+      th_t = std::sqrt(-alpha * alpha * std::log(R(1) - rx));
+      ct = R(1) / std::sqrt(R(1) + th_t * th_t);
+      st = th_t * ct;
+      P::cos_sin_2pi(ry, &cp, &sp);
+    } else {
+      double theta = std::atan(std::sqrt(-alpha * alpha * std::log(1 - rx)));
+      double phi = 2 * PI_D * ry;
+      st = std::sin(theta); ct = std::cos(theta); sp = std::sin(phi); cp = std::cos(phi);
+      th_t = std::tan(theta);
+    }
+    V h(st * cp, st * sp, ct);
+    R costheta = dot(wo, h) / wo.norm();
+    V d = wo - h * costheta * wo.norm();
+    *wi = h * costheta * wo.norm() - d;
+    wi->normalize();
+    if (wo.z <= R(EPS_F) || wi->z <= R(EPS_F)) {
+      *pdf = 1;
+      *wi = V(0, 0, 1);
+      return V();
+    }
+    R p_theta;
+    if (P::kDevEnv) {
+      const R q = th_t / alpha, c2 = ct * ct;
+      p_theta = R(2) * st * std::exp(-(q * q)) / (alpha * alpha * (c2 * ct));
+    } else {
+      double theta = std::atan(std::sqrt(-alpha * alpha * std::log(1 - rx)));
+      p_theta = (R)(2 * std::sin(theta) * std::exp(-std::pow(std::tan(theta) / alpha, 2)) /
+                    (alpha * alpha * std::pow(std::cos(theta), 3)));
+    }
+    R p_phi = R(1.) / (R(2) * R(PI_D));
+    R pdf_h = p_theta * p_phi / st;
+    *pdf = pdf_h / (R(4) * dot(*wi, h));
+    return mf_f(M, wo, *wi);
+  }
+
   V bsdf_f(int m, const V& wo, const V& wi) const {
     const Mat<R>& M = sc.mats[m];
     if (M.type == BDPT_MAT_DIFFUSE) {                                         // bsdf.cpp:52-62
       if (wo.z < 0. || wi.z < 0.) return V();
       return M.a / R(PI_D);
     }
+    if (M.type == BDPT_MAT_MICROFACET) return mf_f(M, wo, wi);              // PathTracer only
     return V();                                      // emission/mirror/glass/refraction f = 0
   }
   V bsdf_sample_f(int m, const V& wo, V* wi, R* pdf) {
@@ -866,6 +963,7 @@ struct Tracer {
         *wi = cosine_hemi(pdf);
         return V();
       }
+      case BDPT_MAT_MICROFACET: return mf_sample_f(M, wo, wi, pdf);            // :89-142
       case BDPT_MAT_MIRROR: {                                                 // advanced_bsdf.cpp:21-29
         reflect(wo, wi);
         *pdf = 1;
@@ -942,8 +1040,8 @@ struct Tracer {
       const EnvMap<R>& E = sc.env;
       R ux, uy;
       grid2d(&ux, &uy);
-      R jx = pol.uS();
-      R jy = pol.uS();
+      R jx = pol.uE();
+      R jy = pol.uE();
       V w;
       R pw;
       V Le = env_sample_dir<P>(E, ux, uy, jx, jy, &w, &pw);
@@ -987,8 +1085,8 @@ struct Tracer {
     if (L.type == LIGHT_ENV_ORC) {   // a vertex at infinity in direction w
       R ux, uy;
       grid2d(&ux, &uy);
-      R jx = pol.uS();
-      R jy = pol.uS();
+      R jx = pol.uE();
+      R jy = pol.uE();
       R pw;
       V Le = env_sample_dir<P>(sc.env, ux, uy, jx, jy, wi, &pw);
       *point = p;
@@ -1054,6 +1152,40 @@ struct Tracer {
     return *dir_pdf > 0. ? L.radiance : V();
   }
 
+  // sample_L (light.cpp:18-23, 103-113, 205-217; environment_light.cpp:126-156): the PathTracer's
+  // next-event estimation. AreaLight's pdf is the solid-angle one; the caller divides by dist^2
+  // once more (pathtracer.cpp:147, the reference's own convention).
+  V light_sample_L(const Light<R>& L, const V& p, V* wi, R* dist, R* pdf) {
+    if (L.type == LIGHT_ENV_ORC) {
+      R ux, uy;
+      grid2d(&ux, &uy);
+      R jx = pol.uE();
+      R jy = pol.uE();
+      *dist = (R)INFINITY;
+      return env_sample_dir<P>(sc.env, ux, uy, jx, jy, wi, pdf);
+    }
+    if (L.type == BDPT_LIGHT_POINT) {
+      V d = L.position - p;
+      *wi = d.unit();
+      *dist = d.norm();
+      *pdf = 1.0;
+      return L.radiance;
+    }
+    R sx, sy;
+    grid2d(&sx, &sy);
+    sx = sx - R(0.5f);
+    sy = sy - R(0.5f);
+    V d = L.position + sx * L.dim_x + sy * L.dim_y - p;
+    R cosTheta = dot(d, L.direction);
+    R sqDist = d.norm2();
+    R dd = std::sqrt(sqDist);
+    *wi = d / dd;
+    *dist = dd;
+    *pdf = sqDist / (L.area * std::fabs(cosTheta));
+    return cosTheta < 0 ? L.radiance : V();
+  }
+  bool light_is_delta(const Light<R>& L) const { return L.type == BDPT_LIGHT_POINT; }
+
   // ---------------- camera (camera.cpp) ----------------
   Ray<R> generate_ray(R x, R y) const {                                       // :191-212
     V rd;
@@ -1069,6 +1201,34 @@ struct Tracer {
     r.max_t = sc.fclip;
     return r;
   }
+  // Camera::generate_ray_for_thin_lens (camera_lens.cpp:22-43)
+  R lens_radius = 0, focal_distance = R(4.7);
+  // uTheta: the lens sample's y; the reference passes rndTheta = uTheta * 2.0 * PI
+  // (pathtracer.cpp:315), mode 2 takes cos/sin(2 pi u) from the device polynomial.
+  Ray<R> generate_ray_thin_lens(R x, R y, R rndR, R uTheta) const {
+    V pLens;
+    if (P::kDevEnv) {
+      R c, s;
+      P::cos_sin_2pi(uTheta, &c, &s);
+      pLens = V(lens_radius * std::sqrt(rndR) * c, lens_radius * std::sqrt(rndR) * s, 0);
+    } else {
+      R rndTheta = uTheta * 2.0 * PI_D;
+      pLens = V(lens_radius * std::sqrt(rndR) * std::cos(rndTheta), lens_radius * std::sqrt(rndR) * std::sin(rndTheta), 0);
+    }
+    V rayDir((2 * x - 1) * tanh_, (2 * y - 1) * tanv_, -1);
+    V pFocus = rayDir * focal_distance;
+    rayDir = pFocus - pLens;
+    V wd = rayDir.x * sc.c2w[0] + rayDir.y * sc.c2w[1] + rayDir.z * sc.c2w[2];
+    wd.normalize();
+    V lo = pLens.x * sc.c2w[0] + pLens.y * sc.c2w[1] + pLens.z * sc.c2w[2];
+    Ray<R> r;
+    r.o = sc.cam_pos + lo;
+    r.d = wd;
+    r.min_t = sc.nclip;
+    r.max_t = sc.fclip;
+    return r;
+  }
+
   V sample_ray_pdf(const V& p, V* wi, V* eye_point, R* dist, R* point_pdf, R* dir_pdf, V* normal,
                    int* x, int* y) const {                                     // :214-248
     *wi = sc.cam_pos - p;
@@ -1301,6 +1461,109 @@ struct Tracer {
       return R(1.) / ((R(1.) + ge) + gl);
     }
     return R(1.) / w_inv;
+  }
+
+  // ---------------- the unidirectional PathTracer (pathtracer.cpp:47-340) ----------------
+  int ns_area_light = 1;
+  bool hemisphere = false;   // direct_hemisphere_sample (-H)
+  V pt_direct_hemisphere(const Ray<R>& r, const Isect& isect) {              // :47-97
+    Frame<R> o2w = make_coord_space(isect.n);
+    const V hit_p = r.o + r.d * isect.t;
+    const V w_out = o2w.to_local(-r.d);
+    int num_samples = (int)sc.lights.size() * ns_area_light;
+    V L_out;
+    for (int i = 0; i < num_samples; i++) {
+      R pdf;
+      V wi, f, wi_world;
+      f = bsdf_sample_f(isect.mat, w_out, &wi, &pdf);
+      wi_world = o2w.to_world(wi);
+      wi_world.normalize();
+      Ray<R> ray;
+      ray.o = hit_p; ray.d = wi_world; ray.min_t = R(EPS_F); ray.max_t = (R)INFINITY;
+      Isect is2;
+      if (!intersect(ray, &is2, true)) continue;
+      R costhetha = std::fabs(dot(wi_world, isect.n));
+      V L_in = get_emission(is2.mat);
+      L_out += L_in * f * costhetha / pdf;
+    }
+    L_out /= R(num_samples);
+    return L_out;
+  }
+  V pt_direct_importance(const Ray<R>& r, const Isect& isect) {              // :99-169
+    Frame<R> o2w = make_coord_space(isect.n);
+    const V hit_p = r.o + r.d * isect.t;
+    const V w_out = o2w.to_local(-r.d);
+    V L_out;
+    for (const Light<R>& light : sc.lights) {
+      int n_samples = light_is_delta(light) ? 1 : ns_area_light;
+      R pdf, distToLight;
+      V wi, f, wi_world, emit_radiance, L_o;
+      for (int i = 0; i < n_samples; i++) {
+        emit_radiance = light_sample_L(light, hit_p, &wi_world, &distToLight, &pdf);
+        wi = o2w.to_local(wi_world);
+        f = bsdf_f(isect.mat, w_out, wi);
+        Ray<R> ray;
+        ray.o = hit_p; ray.d = wi_world; ray.min_t = R(EPS_F); ray.max_t = distToLight - R(EPS_F);
+        Isect is2;
+        if (intersect(ray, &is2, false)) continue;
+        R costhetha = std::fabs(dot(wi_world, isect.n));
+        V L_in = distToLight >= (R)INFINITY ? emit_radiance : emit_radiance / (distToLight * distToLight);
+        L_o += L_in * f * costhetha / pdf;
+      }
+      L_o /= R(n_samples);
+      L_out += L_o;
+    }
+    return L_out;
+  }
+  V pt_at_least_one_bounce(const Ray<R>& r, int depth, const Isect& isect) {   // :181-262
+    Frame<R> o2w = make_coord_space(isect.n);
+    V hit_p = r.o + r.d * isect.t;
+    V w_out = o2w.to_local(-r.d);
+    V L_out, L_o;
+    if (!is_delta(isect.mat)) L_out += hemisphere ? pt_direct_hemisphere(r, isect) : pt_direct_importance(r, isect);
+    bool trace = true, roulette = false;
+    R cpdf = R(0.3);
+    if (max_depth == 0) {
+      roulette = true;
+      if (!(pol.uP() < cpdf) || depth >= 20) trace = false;
+    } else if (depth >= max_depth - 1) {
+      trace = false;
+    }
+    if (!trace) return L_out;
+    V wi, f, wi_world;
+    R pdf;
+    f = bsdf_sample_f(isect.mat, w_out, &wi, &pdf);
+    wi_world = o2w.to_world(wi);
+    wi_world.normalize();
+    Ray<R> ray;
+    ray.o = hit_p; ray.d = wi_world; ray.min_t = R(EPS_F); ray.max_t = (R)INFINITY;
+    Isect is2;
+    if (!intersect(ray, &is2, true)) return L_out;
+    R costhetha = std::fabs(dot(wi_world, isect.n));
+    V L_in = pt_at_least_one_bounce(ray, depth + 1, is2);
+    if (is_delta(isect.mat)) L_in += get_emission(is2.mat);
+    if (roulette) L_o += L_in * f * costhetha / pdf / cpdf;
+    else L_o += L_in * f * costhetha / pdf;
+    L_out += L_o;
+    return L_out;
+  }
+  V pt_est_radiance(const Ray<R>& r) {                                       // :264-290
+    Isect isect;
+    V L_out;
+    if (!intersect(r, &isect, true)) return sc.env_light >= 0 ? env_radiance<P>(sc.env, r.d) : L_out;
+    L_out = get_emission(isect.mat);
+    L_out += pt_at_least_one_bounce(r, 0, isect);
+    return L_out;
+  }
+  // One camera sample of pixel (x, y) (:304-316).
+  V pt_sample(int x, int y) {
+    R px, py, lx, ly;
+    grid2d(&px, &py);
+    px = px + R(x);
+    py = py + R(y);
+    R dx = px / R(W), dy = py / R(H);
+    grid2d(&lx, &ly);
+    return pt_est_radiance(generate_ray_thin_lens(dx, dy, lx, ly));
   }
 
   void splat(int x, int y, const V& s) {
@@ -1572,6 +1835,85 @@ static int env_lookup(const bdpt_scene_desc* d, int n, const double* dirs, doubl
   }
   return 0;
 }
+// PathTracer::raytrace_pixel (pathtracer.cpp:292-338): adaptive batches of camera samples.
+struct PtSettings {
+  int ns_area_light, batch, hemisphere;
+  float tol;
+  double lens_radius, focal_distance;
+};
+template <class P>
+static void pt_pixel(Tracer<P>& tr, int x, int y, int ns_aa, const PtSettings& ps, CounterStream* cs,
+                     uint64_t seed, double* out, int* count) {
+  typedef typename P::R R;
+  int num_samples = 0;
+  V3<R> illumination(0, 0, 0);
+  R s1 = 0, s2 = 0;
+  for (int i = 0; i < ns_aa; i = i + ps.batch) {
+    for (int j = 0; j < ps.batch; j++) {
+      if (cs) cs->init(seed, (uint32_t)(x + y * tr.W), (uint32_t)(i + j));
+      V3<R> ill = tr.pt_sample(x, y);
+      illumination += ill;
+      R il;
+      if (sizeof(R) == 8) il = (float)(0.2126f * ill.x + 0.7152f * ill.y + 0.0722f * ill.z);   // illum() is float
+      else il = R(0.2126f) * ill.x + R(0.7152f) * ill.y + R(0.0722f) * ill.z;
+      s1 += il;
+      s2 += il * il;
+    }
+    num_samples = i + ps.batch;
+    R mu = s1 / R(num_samples);
+    R sigma = std::sqrt((s2 - s1 * s1 / R(num_samples)) / R(num_samples - 1));
+    R ci = R(1.96) * sigma / std::sqrt(R(num_samples));
+    if (ci <= R((double)ps.tol) * mu && mu > R(EPS_F)) break;
+  }
+  illumination /= R(num_samples);
+  for (int c = 0; c < 3; c++) out[c] = (double)illumination[c];
+  *count = num_samples;
+}
+
+template <class R>
+static int pt_render_counter(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, uint64_t seed,
+                             const PtSettings& ps, int nthreads, double* image, int* counts, double* stats) {
+  Scene<R> sc;
+  std::string err;
+  int rc = load_scene<R>(d, sc, err, true);
+  if (rc) { fprintf(stderr, "oracle: %s\n", err.c_str()); return rc; }
+  if (nthreads < 1) nthreads = 1;
+  std::vector<Stats> sts(nthreads);
+  typedef typename std::conditional<sizeof(R) == 8, PolicyC64, PolicyC32>::type P;
+  auto work = [&](int t) {
+    CounterStream cs;
+    cs.init(seed, 0, 0);
+    P pol;
+    pol.cs = &cs;
+    Tracer<P> tr(sc, pol, max_depth, W, H, spp);
+    tr.ns_area_light = ps.ns_area_light;
+    tr.hemisphere = ps.hemisphere != 0;
+    tr.lens_radius = (R)ps.lens_radius;
+    tr.focal_distance = (R)ps.focal_distance;
+    for (int y = t; y < H; y += nthreads)
+      for (int x = 0; x < W; x++) {
+        size_t k = (size_t)x + (size_t)y * W;
+        pt_pixel(tr, x, y, spp, ps, &cs, seed, image + 3 * k, counts + k);
+      }
+    sts[t] = tr.st;
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+  if (stats) {
+    Stats S;
+    for (auto& q : sts) {
+      S.rays += q.rays; S.closest += q.closest; S.shadow += q.shadow; S.nodes += q.nodes;
+      S.tri += q.tri; S.sph += q.sph; S.hits += q.hits;
+    }
+    stats[0] = (double)S.rays; stats[1] = (double)S.closest; stats[2] = (double)S.shadow;
+    stats[3] = (double)S.nodes; stats[4] = (double)S.tri; stats[5] = (double)S.sph;
+    stats[6] = (double)S.hits; stats[7] = (double)sc.nodes.size();
+  }
+  return 0;
+}
+
 }  // namespace orc
 
 using namespace orc;
@@ -1652,6 +1994,49 @@ int oracle_env_sample(const bdpt_scene_desc* d, int mode, int n, const double* u
 int oracle_env_lookup(const bdpt_scene_desc* d, int mode, int n, const double* dirs, double* rad, double* pdf) {
   if (mode == 2) return env_lookup<PolicyC32>(d, n, dirs, rad, pdf);
   return env_lookup<PolicyC64>(d, n, dirs, rad, pdf);
+}
+
+// The unidirectional PathTracer (pathtracer.cpp:47-340). mode 0: the
+// reference's own sequence (its four TU-static engines, tiles of 32 in raster order, -t 1); modes
+// 1/2: counter RNG keyed by (pixel, sample index within the pixel). image: W*H*3 (row 0 = bottom)
+// = sampleBuffer, counts: W*H = sampleCountBuffer.
+int oracle_pt_render(const bdpt_scene_desc* d, int W, int H, int spp, int max_depth, int mode, uint64_t seed,
+                     int ns_area_light, int samples_per_batch, float max_tolerance, int hemisphere,
+                     double lens_radius, double focal_distance, int nthreads, double* image, int* counts,
+                     double* stats) {
+  if (!d || W <= 0 || H <= 0 || spp <= 0 || max_depth < 0 || samples_per_batch <= 0 || ns_area_light <= 0)
+    return BDPT_E_INVALID;
+  PtSettings ps{ns_area_light, samples_per_batch, hemisphere, max_tolerance, lens_radius, focal_distance};
+  if (mode == 1) return pt_render_counter<double>(d, W, H, spp, max_depth, seed, ps, nthreads, image, counts, stats);
+  if (mode == 2) return pt_render_counter<float>(d, W, H, spp, max_depth, seed, ps, nthreads, image, counts, stats);
+  if (mode != 0) return BDPT_E_INVALID;
+  Scene<double> sc;
+  std::string err;
+  int rc = load_scene<double>(d, sc, err, true);
+  if (rc) { fprintf(stderr, "oracle: %s\n", err.c_str()); return rc; }
+  RefStreams rs;
+  std::srand(1);
+  PolicyRef pol;
+  pol.rs = &rs;
+  Tracer<PolicyRef> tr(sc, pol, max_depth, W, H, spp);
+  tr.ns_area_light = ns_area_light;
+  tr.hemisphere = hemisphere != 0;
+  tr.lens_radius = lens_radius;
+  tr.focal_distance = focal_distance;
+  const int TS = 32;
+  for (int ty = 0; ty < H; ty += TS)
+    for (int tx = 0; tx < W; tx += TS)
+      for (int y = ty; y < std::min(ty + TS, H); y++)
+        for (int x = tx; x < std::min(tx + TS, W); x++) {
+          size_t k = (size_t)x + (size_t)y * W;
+          pt_pixel(tr, x, y, spp, ps, nullptr, seed, image + 3 * k, counts + k);
+        }
+  if (stats) {
+    stats[0] = (double)tr.st.rays; stats[1] = (double)tr.st.closest; stats[2] = (double)tr.st.shadow;
+    stats[3] = (double)tr.st.nodes; stats[4] = (double)tr.st.tri; stats[5] = (double)tr.st.sph;
+    stats[6] = (double)tr.st.hits; stats[7] = (double)sc.nodes.size();
+  }
+  return 0;
 }
 
 // BVH facts of the oracle's reference build: nodes, depth, DFS leaf order (prim indices).

@@ -233,13 +233,15 @@ static HDRImageBuffer* load_exr(const char* file_path) {
 }
 
 int main(int argc, char** argv) {
-  size_t ns_aa = 1, max_depth = 1, threads = 1, w = 0, h = 0, batch = 32;
+  size_t ns_aa = 1, max_depth = 1, threads = 1, w = 0, h = 0, batch = 32, nal = 1;
   float tol = 0.05f;
+  bool hemi = false;
+  double lens = 0.0, focal = 4.7;
   std::string png = "/dev/null", npy_prefix, scene_json;
   bool render = true, uni = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -251,6 +253,10 @@ int main(int argc, char** argv) {
       case 'n': render = false; break;
       case 'e': envmap = load_exr(optarg); if (!envmap) return 4; break;
       case 'U': uni = true; break;
+      case 'H': hemi = true; break;                      // main.cpp:138-141
+      case 'l': nal = atoi(optarg); break;               // main.cpp:107-109
+      case 'b': lens = atof(optarg); break;              // main.cpp:128-130
+      case 'd': focal = atof(optarg); break;             // main.cpp:131-133
       case 'a': batch = atoi(argv[optind - 1]); tol = atof(argv[optind]); optind++; break;   // main.cpp:134-137
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
@@ -324,8 +330,8 @@ int main(int argc, char** argv) {
   if (w && h) { screenW = w; screenH = h; camera.set_screen_size(w, h); }
 
   // --- Application ctor (application.cpp:21-40) with AppConfig defaults (application.h:45-65) ---
-  RaytracedRenderer* rr = new RaytracedRenderer(ns_aa, max_depth, 1, 1, 1, 1, threads, batch, tol,
-                                                envmap, false, "", 0.0, 4.7);
+  RaytracedRenderer* rr = new RaytracedRenderer(ns_aa, max_depth, nal, 1, 1, 1, threads, batch, tol,
+                                                envmap, hemi, "", lens, focal);
   if (uni) {   // the reference's unidirectional integrator with the same settings (:53-74)
     PathTracer* u = new PathTracer();
     PathTracer* b = rr->pt;
@@ -344,6 +350,11 @@ int main(int argc, char** argv) {
   rr->render_to_file(png, (size_t)-1, 0, 0, 0);
   if (!npy_prefix.empty() && uni) {
     write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);
+    FILE* fc = fopen((npy_prefix + "_count.bin").c_str(), "wb");   // sampleCountBuffer, int32 row-major
+    if (fc) {
+      fwrite(rr->pt->sampleCountBuffer.data(), sizeof(int), rr->pt->sampleCountBuffer.size(), fc);
+      fclose(fc);
+    }
   } else if (!npy_prefix.empty()) {
     BidirectionalPathTracer* pt = (BidirectionalPathTracer*)rr->pt;
     write_npy(npy_prefix + "_sample.npy", pt->sampleBuffer);

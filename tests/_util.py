@@ -35,6 +35,9 @@ def oracle():
         lib.oracle_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, P, P, P, P]
         lib.oracle_render_ex.argtypes = lib.oracle_render.argtypes + [C.c_int]
+        lib.oracle_pt_render.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_float, C.c_int,
+                                         C.c_double, C.c_double, C.c_int, P, C.POINTER(C.c_int), P]
         lib.oracle_env_tables.argtypes = [C.POINTER(B.SceneDesc), P, P, P]
         lib.oracle_env_sample.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, P, P, P, P]
         lib.oracle_env_lookup.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.c_int, P, P, P]
@@ -78,6 +81,25 @@ def oracle_render(scene, W, H, spp, max_depth, mode, seed=5489, s0=0, count=None
     if mode != MODE_REF:
         samp = eye + light
     return samp, eye, light, st
+
+
+def oracle_pt_render(scene, W, H, spp, max_depth, mode, seed=5489, ns_area_light=1, batch=32, tol=0.05,
+                     hemisphere=False, lens_radius=0.0, focal_distance=4.7, threads=None):
+    """The oracle's unidirectional PathTracer (pathtracer.cpp): (image (H, W, 3) = sampleBuffer,
+    counts (H, W) = sampleCountBuffer, stats)."""
+    lib = oracle()
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    img = np.zeros((H, W, 3))
+    cnt = np.zeros((H, W), dtype=np.int32)
+    st = np.zeros(8)
+    d = scene.desc()
+    rc = lib.oracle_pt_render(C.byref(d), W, H, spp, max_depth, mode, seed, ns_area_light, batch, tol,
+                              1 if hemisphere else 0, lens_radius, focal_distance, threads, _p(img),
+                              cnt.ctypes.data_as(C.POINTER(C.c_int)), _p(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_pt_render rc={rc}")
+    return img, cnt, st
 
 
 def golden_scene(name, width=None, height=None):

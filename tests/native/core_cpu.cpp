@@ -112,3 +112,49 @@ extern "C" int core_cpu_scene_info(const bdpt_scene_desc* d, int* depth, int* re
   for (size_t i = 0; i < hs.ref_order.size(); i++) prim_ref[i] = hs.ref_order[i];
   return 0;
 }
+
+// The unidirectional PathTracer (bdpt_core.h pt_pixel) for the whole frame: image = W*H*3
+// (sampleBuffer), counts = W*H (sampleCountBuffer).
+extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed,
+                                  int ns_area_light, int batch, float tol, int hemisphere, double lens,
+                                  double focal, double* image, int* counts) {
+  HostScene hs;
+  std::string err;
+  int rc = build_host_scene(d, hs, err, true);
+  if (rc) { fprintf(stderr, "core_cpu: %s\n", err.c_str()); return rc; }
+  SceneView S;
+  const HostBvh& T = hs.tree(lm_width(0));
+  S.nodes = (const float4*)T.nodes.data();
+  S.geom = (const float4*)hs.geom.data();
+  S.shade = (const float4*)hs.shade.data();
+  S.mats = hs.mats.data();
+  S.lights = hs.lights.data();
+  S.nlights = (int)hs.lights.size();
+  S.root = T.root;
+  S.lnodes = nullptr;
+  S.lgeom = nullptr;
+  S.ntop = 0;
+  S.cam = hs.cam;
+  const size_t np = (size_t)hs.env_w * hs.env_h;
+  S.env.light = hs.env_light;
+  S.env.w = hs.env_w;
+  S.env.h = hs.env_h;
+  S.env.marg = hs.env.data();
+  S.env.cond = hs.env.data() + hs.env_h;
+  S.env.pdf = hs.env.data() + hs.env_h + np;
+  S.env.rgb = hs.env.data() + hs.env_h + 2 * np;
+  S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];
+  S.env.rad = hs.env_rad;
+  PtParams pp;
+  pp.W = W; pp.H = H; pp.spp = spp; pp.max_depth = M; pp.seed = seed;
+  pp.ns_area_light = ns_area_light; pp.batch = batch; pp.hemisphere = hemisphere; pp.tol = tol;
+  pp.lens_radius = (float)lens; pp.focal_distance = (float)focal;
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      const size_t k = (size_t)x + (size_t)y * W;
+      const f3 v = pt_pixel<0>(S, pp, cnt, x, y, counts + k);
+      image[3 * k] = v.x; image[3 * k + 1] = v.y; image[3 * k + 2] = v.z;
+    }
+  return 0;
+}

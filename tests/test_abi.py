@@ -31,7 +31,7 @@ def test_library_exports_every_declared_function():
 
 
 def test_abi_version():
-    assert B.load_library().bdpt_abi_version() == 2   # v2: envmap + russian_roulette
+    assert B.load_library().bdpt_abi_version() == 3   # v2: envmap + russian_roulette; v3: integrator
 
 
 def test_null_arguments_rejected():

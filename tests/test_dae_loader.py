@@ -16,7 +16,7 @@ SCENES = os.path.join(REPO, "scenes")
 
 
 @pytest.mark.parametrize("name", ["CBspheres", "CBspheres_lambertian", "CBspheres_refract", "CBgems",
-                                  "CBempty"])
+                                  "CBempty", "CBspheres_microfacet_al_ag"])
 def test_loader_bit_exact_vs_reference_loader(name, tmp_path):
     out = tmp_path / f"{name}.json"
     with open(os.path.join(GOLD, "scenes", name + ".json")) as f:
