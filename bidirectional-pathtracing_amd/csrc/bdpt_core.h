@@ -1539,8 +1539,10 @@ struct Conn {
 // A vertex that can receive a connection: diffuse (f != 0 only for DiffuseBSDF, bsdf.cpp:52-62),
 // viewed from its front side (wo.z >= 0) and carrying throughput.
 BDPT_HD bool can_connect(const Vtx& v) { return v.cq > 0.0f; }
+// ev_pre: E[i] already loaded by the caller (the megakernel's j loop reuses it), or null.
 template <bool EXT = false, class PA>
-BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn) {
+BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn,
+                      const Vtx* ev_pre = nullptr) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   const bool eye_cam = i == 1;
   Vtx ev, lv;
@@ -1549,7 +1551,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
   EyeSample es;
   es.x = -1; es.y = -1;
   cn.splat = -1;
-  if (!eye_cam) ev = P.e(i);
+  if (!eye_cam) ev = ev_pre ? *ev_pre : P.e(i);
   if (j == 0) {
     if (eye_cam) return CONN_NONE;
     if (EXT && is_env(ev)) {   // an escaped eye ray: the environment light contains it (§9)
