@@ -247,9 +247,10 @@ __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int h
 #endif
 constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
 
-// E[i] loaded once per i for all j (instead of once per (i, j) connection).
-#ifndef BDPT_HOIST_EV
-#define BDPT_HOIST_EV 0
+// Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
+// wave-uniform max|E| x max|L| grid (the special strategies stay wave-uniform).
+#ifndef BDPT_CONN_COMPACT
+#define BDPT_CONN_COMPACT 0
 #endif
 // Materials and lights copied to LDS (static arrays) when they fit: per-lane material / light
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
@@ -361,20 +362,13 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       ph_prep += tp1 - tp0;
       unsigned long long tg0 = tp1;
   #endif
-      for (int i = 1; i < wE; i++) {
-#if BDPT_HOIST_EV
-      Vtx evh;   // E[i], read from scratch once for the whole j loop
-      if (i >= 2 && i < nE) evh = P.E[i - 2];
-#endif
-      for (int j = 0; j < wL; j++) {
+      // one (i, j) connection per lane (active lanes only), its ray pushed into the wave's ring,
+      // the ring flushed whenever 64 rays are queued
+      auto conn_step = [&](int i, int j, bool active) {
         int kind = CONN_NONE;
         Conn cn;
-        if (i < nE && j < nL) {
-#if BDPT_HOIST_EV
-          kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn, i >= 2 ? &evh : nullptr);
-#else
+        if (active) {
           kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn);
-#endif
           if (kind == CONN_DIRECT) {
             dxs += cn.val.x * inv;
             dys += cn.val.y * inv;
@@ -413,8 +407,34 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
           ph_flush += tp1 - tp0;
   #endif
         }
+      };
+#if BDPT_CONN_COMPACT
+      // The special strategies wave-uniformly: s = 0 (j = 0), the fresh light sample (j = 1),
+      // light tracing to the camera (i = 1, j >= 2) ...
+      for (int i = 2; i < wE; i++) conn_step(i, 0, i < nE);
+      for (int i = 1; i < wE; i++) conn_step(i, 1, i < nE && nL > 1);
+      for (int j = 2; j < wL; j++) conn_step(1, j, j < nL);
+      // ... then the general (i >= 2, j >= 2) pairs from per-lane lists of connectable vertices:
+      // a lane walks its own (i, j) pairs, so the wave iterates max(pairs) times instead of
+      // max|E| x max|L| (most cells of that grid are empty for most lanes)
+      unsigned mE = 0, mL = 0;
+      for (int k = 2; k < nE; k++) mE |= (P.E[k - 2].cq > 0.0f ? 1u : 0u) << k;
+      for (int k = 2; k < nL; k++) mL |= (P.L[k - 1].cq > 0.0f ? 1u : 0u) << k;
+      if (mL == 0) mE = 0;
+      unsigned jm = mL;
+      while (__ballot(mE != 0)) {
+        const bool act = mE != 0;
+        const int ci = act ? __builtin_ctz(mE) : 0, cj = act ? __builtin_ctz(jm) : 0;
+        conn_step(ci, cj, act);
+        if (act) {
+          jm &= jm - 1;
+          if (jm == 0) { mE &= mE - 1; jm = mL; }
+        }
       }
-      }
+#else
+      for (int i = 1; i < wE; i++)
+      for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
+#endif
   #ifdef BDPT_PHASE_PROF
       ph_gen += __builtin_amdgcn_s_memtime() - tg0;
   #endif
