@@ -135,6 +135,10 @@ def main() -> int:
                     help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
                          "synthetic sky of tools/envmap.py (the reference's exr/*.exr are LFS pointers)")
     ap.add_argument("--rr", action="store_true", help="Russian roulette on both subpaths")
+    ap.add_argument("--integrator", choices=["bdpt", "pt"], default="bdpt",
+                    help="bdpt (the reference's BidirectionalPathTracer, the headline) or pt (its "
+                         "unidirectional PathTracer, DESIGN.md §10; adaptive sampling off: every "
+                         "pixel takes all spp; ranks split the frame into row bands)")
     args = ap.parse_args()
     W, H, SPP, M = args.width, args.height, args.spp, args.max_depth
 
@@ -172,14 +176,25 @@ def main() -> int:
     stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
     torch.cuda.set_stream(stream)
     # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
-    pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                   pipeline=args.pipeline, russian_roulette=args.rr)
+    use_pt = args.integrator == "pt"
+    band = [(0, H * rank // world, W, H * (rank + 1) // world - H * rank // world)]
+    if use_pt:   # whole pixels: each rank renders its row band with all SPP samples
+        pt = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index, max_tolerance=0.0)
+    else:
+        pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
+                                       pipeline=args.pipeline, russian_roulette=args.rr)
     pt.set_stream(stream.cuda_stream)
     frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
 
+    def render(k: int):
+        if use_pt:
+            pt.raytrace_tiles(band, 0, SPP)
+        else:
+            base, n = rank_sample_range(k, rank, world, SPP)   # fresh global sample range every step
+            pt.raytrace_tiles([], base, n)
+
     def step(k: int):
-        base, n = rank_sample_range(k, rank, world, SPP)   # fresh global sample range every step
-        pt.raytrace_tiles([], base, n)
+        render(k)
         pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
         if dist is not None:
             dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
@@ -194,9 +209,8 @@ def main() -> int:
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
-        base, n = rank_sample_range(args.warmup + k, rank, world, SPP)
         ev[k][0].record(stream)
-        pt.raytrace_tiles([], base, n)              # k_bdpt_sample: the dominant kernel
+        render(args.warmup + k)                     # k_bdpt_sample (k_pt): the dominant kernel
         ev[k][1].record(stream)
         pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
         if dist is not None:
@@ -207,6 +221,8 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rank_samples = int(pt.read_sample_counts().astype(np.int64)[band[0][1]:band[0][1] + band[0][3]].sum()) \
+        if use_pt else W * H * SPP
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -215,18 +231,29 @@ def main() -> int:
 
     # algorithmic bytes of one launch: in-kernel counters on a separate, untimed launch of the
     # same workload (counting perturbs timing), SURVEY.md §8d.
-    ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                   collect_stats=True, pipeline=args.pipeline, russian_roulette=args.rr)
-    ps.raytrace_tiles([], rank * SPP, SPP)
+    if use_pt:
+        ps = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index, max_tolerance=0.0,
+                          collect_stats=True)
+        ps.raytrace_tiles(band, 0, SPP)
+    else:
+        ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
+                                       collect_stats=True, pipeline=args.pipeline, russian_roulette=args.rr)
+        ps.raytrace_tiles([], rank * SPP, SPP)
     st = ps.stats()
     ps.close()
     bytes_launch = algorithmic_bytes(st)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
-    samples_total = W * H * SPP * world * args.steps
+    if dist is not None and use_pt:
+        t = torch.tensor([rank_samples], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        samples_total = float(t.item()) * args.steps
+    else:
+        samples_total = (rank_samples if use_pt else W * H * SPP * world) * args.steps
     value = samples_total / elapsed / 1e6
     traffic = None
-    default_workload = (args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5) and not args.envmap and not args.rr
+    default_workload = ((args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5) and not args.envmap
+                        and not args.rr and not use_pt)
     tpath = os.path.join(REPO, "profiles", "traffic_r01.json")   # PMC pass of this workload
     if default_workload and os.path.exists(tpath):
         with open(tpath) as f:
@@ -252,6 +279,7 @@ def main() -> int:
                 f"{os.path.basename(args.scene)} as the reference loads it",
         "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} -s {SPP} -m {M}"
                                f"{' + env ' + env_desc if env_desc else ''}{' RR on' if args.rr else ''}"
+                               f"{' unidirectional PathTracer' if use_pt else ''}"
                                f"{' (BASELINE configs[1])' if default_workload else ''} "
                                f"per GPU, sample-range shards + RCCL sum-reduce",
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
@@ -260,16 +288,21 @@ def main() -> int:
                    "parallelism": f"samples x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                     "traffic": traffic, "kernel": "k_bdpt_sample", "kernel_ms": round(kern_ms, 3),
+                     "traffic": traffic, "kernel": "k_pt" if use_pt else "k_bdpt_sample",
+                     "kernel_ms": round(kern_ms, 3),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "counts_per_launch": {"node_aabbs": st.node_visits, "tri_tests": st.tri_tests,
                                            "sph_tests": st.sph_tests, "hits": st.hits,
                                            "closest_rays": st.closest_rays,
                                            "shadow_rays": st.shadow_rays}},
     }
-    if world == 1 and not args.no_parity:
+    if use_pt:
+        out["config"]["integrator"] = "PathTracer (pathtracer.cpp:47-340)"
+        out["config"]["parallelism"] = f"row bands x{world}"
+        out["scaling"] = "strong"
+    if world == 1 and not args.no_parity and not use_pt:
         out["parity"] = parity_check(scene, seed, rr=args.rr)
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not use_pt:
         thr = min(16, os.cpu_count() or 1)
         dae = args.scene if args.scene.endswith(".dae") else os.path.join(REPO, "scenes", args.scene + ".dae")
         port = cpu_baseline(scene, args.scene, threads=thr, rr=args.rr)
