@@ -20,7 +20,7 @@ if os.environ.get("BDPT_LIB"):
     B.load_library(os.environ["BDPT_LIB"])
     B._lib = B.load_library(os.environ["BDPT_LIB"])
 sc = B.load_dae(scene, W, H) if scene.endswith(".dae") else golden_scene(scene, W, H)
-pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489,
+pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489, samples_per_lane=int(os.environ.get("BDPT_SPL", "0")),
                                collect_stats=os.environ.get("BDPT_STATS") == "1")
 if os.environ.get("BDPT_WARM", "1") == "1":   # code-object load + first-launch setup, untimed
     pt.raytrace_tiles([], 0, 1)
