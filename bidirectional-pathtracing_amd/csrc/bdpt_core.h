@@ -251,7 +251,9 @@ struct SceneView {
   int nlights;
   int root;              // root child reference
   const float4* lnodes;  // LDS copy of nodes [0, ntop) (LM 1: all nodes; LM 2: BFS treelet)
-  const float4* lgeom;   // LDS copy of the geometry (LM 1 only)
+  const float4* lgeom;   // LDS copy of the geometry (LM 1 and 3)
+  const int* lleaves;    // LM 3: every leaf reference (LDS), nleaves of them
+  int nleaves;
   int ntop;
   DCam cam;
   EnvView env;
@@ -369,7 +371,9 @@ namespace bdpt {
 #endif
 static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
               "BVH widths must be 2 or 4");
-BDPT_HD constexpr int lm_width(int LM) { return LM == 1 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
+// LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
+// in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
+BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
 BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
 BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
@@ -459,7 +463,14 @@ BDPT_HD float4 ld_glb4(const float4* p) {
 // geometry record k (3 float4 per primitive): LDS copy in LDS mode 1, else HBM
 template <int LM>
 BDPT_HD float4 ld_geom(const SceneView& S, int k) {
-  return LM == 1 ? ld_lds4(S.lgeom + k) : ld_glb4(S.geom + k);
+  return LM == 1 || LM == 3 ? ld_lds4(S.lgeom + k) : ld_glb4(S.geom + k);
+}
+BDPT_HD int ld_lds_i(const int* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(3))) int*)p;
+#else
+  return *p;
+#endif
 }
 // A node from the LDS copy: one asm block of ds_read_b128 and a single wait. Written out because a
 // node fetch that may come from LDS or HBM (treelet mode) otherwise compiles to flat_load for both.
@@ -602,7 +613,12 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.closest++;
+  int li = 0;
   for (;;) {
+    if (LM == 3) {
+      if (li >= S.nleaves) break;
+      ref = ld_lds_i(S.lleaves + li++);
+    }
     while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
     if (ref == kTravDone) break;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
@@ -627,7 +643,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
       }
     }
-    if (!stk.pop(ref)) break;
+    if (LM != 3 && !stk.pop(ref)) break;
   }
   if (h.prim >= 0) c.hits++;
   return h.prim >= 0;
@@ -641,7 +657,12 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.shadow++;
+  int li = 0;
   for (;;) {
+    if (LM == 3) {
+      if (li >= S.nleaves) return false;
+      ref = ld_lds_i(S.lleaves + li++);
+    }
     while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
@@ -658,7 +679,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       }
       if (ok) return true;
     }
-    if (!stk.pop(ref)) return false;
+    if (LM != 3 && !stk.pop(ref)) return false;
   }
 }
 

@@ -35,6 +35,7 @@ struct Ctx {
   DMat* d_mats = nullptr;
   DLight* d_lights = nullptr;
   int* d_prim_ref = nullptr;
+  int* d_leaves = nullptr;     // HostScene::leaf_refs (LM 3 staging source)
   float* d_env = nullptr;      // HostScene::env (environment light tables + map)
   int* d_count = nullptr;      // PathTracer::sampleCountBuffer (W*H)
   bool pt = false;             // bdpt_params.integrator == BDPT_INTEGRATOR_PT
@@ -74,6 +75,8 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.root = c->hs.tree(W).root;
   S.lnodes = nullptr;
   S.lgeom = nullptr;
+  S.lleaves = c->d_leaves;
+  S.nleaves = (int)c->hs.leaf_refs.size();
   S.ntop = 0;
   S.cam = c->hs.cam;
   const HostScene& hs = c->hs;

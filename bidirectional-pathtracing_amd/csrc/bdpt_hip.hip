@@ -277,10 +277,15 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   WaveQ& q = qs[threadIdx.x >> 6];
   if (LM != 0) {
     float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
-    const int nn = LM == 1 ? kp.n_node4 : node_f4(lm_width(LM)) * kp.S.ntop;
-    const int n4 = nn + (LM == 1 ? kp.n_geom4 : 0);
+    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
+    const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
       sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
+    if (LM == 3) {
+      int* lv = (int*)(sc + n4);
+      for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
+      kp.S.lleaves = lv;
+    }
     __syncthreads();
     kp.S.lnodes = sc;
     kp.S.lgeom = sc + nn;
@@ -573,6 +578,11 @@ __global__ void k_combine(const float* a, const float* b, float* out, long long 
 // LDS budget for the scene copy: 160 KB per CU shared by the blocks that the 4-waves/SIMD VGPR
 // budget admits (16 waves per CU), minus their wave queues.
 constexpr size_t kLdsPerCu = 160 * 1024;
+// scenes up to this many primitives use the flat leaf-list traversal (LM 3)
+#ifndef BDPT_FLAT_MAX_PRIMS
+#define BDPT_FLAT_MAX_PRIMS 24   // measured: CBspheres 488 -> 511 Msamples/s, CBspheres_lambertian +6%, CBempty -1%
+#endif
+constexpr int kFlatMaxPrims = BDPT_FLAT_MAX_PRIMS;
 constexpr size_t kBlocksPerCu = 16 / kWavesPerBlock;
 constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256 - kStaticLds;
 
@@ -595,13 +605,18 @@ int launch_lm(Ctx* c, KParams& kp) {
   const size_t q = kWavesPerBlock * sizeof(WaveQ);
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const bool has_nodes = !c->hs.bvh2.nodes.empty();
-  const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2
-  int lm = env ? atoi(env) : (full <= kLdsSceneMax ? 1 : has_nodes ? 2 : 0);
+  const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2 / 3
+  const size_t flat = c->hs.geom.size() * sizeof(float) + c->hs.leaf_refs.size() * sizeof(int);
+  int lm = env ? atoi(env)
+               : (c->hs.nprim <= kFlatMaxPrims && flat <= kLdsSceneMax) ? 3
+               : (full <= kLdsSceneMax ? 1 : has_nodes ? 2 : 0);
+  if (lm == 3 && flat > kLdsSceneMax) lm = 1;
   if (lm == 1 && full > kLdsSceneMax) lm = 2;
   if (lm == 2 && !has_nodes) lm = 0;
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
+  if (lm == 3) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 3, EXT>, q + flat, kp);
   if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, q + full, kp);
   if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
   return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0, EXT>, q, kp);
@@ -642,7 +657,7 @@ int launch_pt(Ctx* c, PtKParams& kp) {
 
 void free_ctx(Ctx* c) {
   if (!c) return;
-  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count,
+  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count, c->d_leaves,
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -719,6 +734,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if ((rc = upload(&c->d_mats, c->hs.mats))) return fail(rc);
   if ((rc = upload(&c->d_lights, c->hs.lights))) return fail(rc);
   if ((rc = upload(&c->d_prim_ref, c->hs.prim_ref))) return fail(rc);
+  if ((rc = upload(&c->d_leaves, c->hs.leaf_refs))) return fail(rc);
   if (c->hs.env_light >= 0 && (rc = upload(&c->d_env, c->hs.env))) return fail(rc);
   c->npix = (size_t)p.width * p.height;
   size_t fb = c->npix * 3 * sizeof(float);

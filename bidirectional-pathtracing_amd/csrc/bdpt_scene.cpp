@@ -523,6 +523,17 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
       }
     }
     B.root = ref_of(root);
+    if (W == 2) {   // every leaf reference in DFS order: the flat traversal of tiny scenes (LM 3)
+      out.leaf_refs.clear();
+      std::vector<int> st{root};
+      while (!st.empty()) {
+        const int id = st.back();
+        st.pop_back();
+        if (T.nodes[id].l < 0) { out.leaf_refs.push_back(ref_of(id)); continue; }
+        st.push_back(T.nodes[id].r);
+        st.push_back(T.nodes[id].l);
+      }
+    }
   }
   return BDPT_OK;
 }

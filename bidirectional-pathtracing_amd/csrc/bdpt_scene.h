@@ -36,6 +36,7 @@ struct HostScene {
   std::vector<float> geom;    // 12 floats per prim
   std::vector<float> shade;   // 12 floats per prim
   std::vector<int32_t> prim_ref;    // device DFS position -> scene primitive index
+  std::vector<int32_t> leaf_refs;   // every leaf of the device tree (encoded refs, DFS order)
   std::vector<int32_t> ref_order;   // the reference tree's DFS leaf order (scene indices)
   std::vector<DMat> mats;
   std::vector<DLight> lights;

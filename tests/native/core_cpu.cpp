@@ -32,7 +32,9 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.root = T.root;
   // LM 1 reads the "LDS copy": on the CPU the same arrays (exercises the LDS-mode tree)
   S.lnodes = LM == 1 ? S.nodes : nullptr;
-  S.lgeom = LM == 1 ? S.geom : nullptr;
+  S.lgeom = LM == 1 || LM == 3 ? S.geom : nullptr;
+  S.lleaves = hs.leaf_refs.data();
+  S.nleaves = (int)hs.leaf_refs.size();
   S.ntop = 0;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
@@ -99,6 +101,7 @@ extern "C" int core_cpu_render(const bdpt_scene_desc* d, int W, int H, int spp, 
                                int count, const int* pixels, int npix, double* eye, double* light, double* stats,
                                int lds_mode, int rr) {
   if (lds_mode == 1) return render_lm<1>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  if (lds_mode == 3) return render_lm<3>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   return render_lm<0>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
 }
 
@@ -133,6 +136,8 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
   S.root = T.root;
   S.lnodes = nullptr;
   S.lgeom = nullptr;
+  S.lleaves = nullptr;
+  S.nleaves = 0;
   S.ntop = 0;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;

@@ -52,10 +52,11 @@ CASES = [("CBspheres", 32, 24, 2, 5), ("CBspheres_lambertian", 32, 24, 2, 5), ("
          ("CBspheres", 24, 18, 3, 1)]
 
 
-@pytest.mark.parametrize("lds_mode", [0, 1])
+@pytest.mark.parametrize("lds_mode", [0, 1, 3])
 @pytest.mark.parametrize("name,W,H,spp,M", CASES)
 def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M, lds_mode):
-    """lds_mode 0 traverses the 4-wide tree (HBM kernels), 1 the binary one (scene in LDS)."""
+    """lds_mode 0 traverses the 4-wide tree (HBM kernels), 1 the binary one (scene in LDS), 3 the
+    flat leaf list (tiny scenes)."""
     sc = golden_scene(name, W, H)
     eye, light, st = core_render(sc, W, H, spp, M, seed=1234, lds_mode=lds_mode)
     _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=1234, threads=1)

@@ -159,7 +159,7 @@ def _with_env(sc, w=64, h=32):
     return sc
 
 
-@pytest.mark.parametrize("lds", ["0", "1", "2"])
+@pytest.mark.parametrize("lds", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("name,W,H,S,M,rr,env", [
     ("CBspheres_lambertian", 128, 96, 4, 5, False, True),
     ("CBspheres", 128, 96, 4, 8, True, True),
@@ -167,7 +167,8 @@ def _with_env(sc, w=64, h=32):
     ("CBempty", 96, 72, 4, 5, True, True),
 ])
 def test_parity_env_rr_vs_oracle(name, W, H, S, M, rr, env, lds, monkeypatch):
-    """EXT megakernel (every LDS mode: scene in HBM, whole scene in LDS, BFS treelet) vs mode 2."""
+    """EXT megakernel (every LDS mode: scene in HBM, whole scene in LDS, BFS treelet, flat leaf
+    list) vs mode 2."""
     monkeypatch.setenv("BDPT_LDS_MODE", lds)
     sc = golden_scene(name, W, H)
     if env:
@@ -247,3 +248,15 @@ def test_pathtracer_env_and_tiles():
         pt.close()
     o_img = oracle_pt_render(sc, W, H, S, M, MODE_C32, seed=3, batch=4)[0]
     assert _rmse(img, o_img) < RMSE_TOL
+
+
+@pytest.mark.parametrize("lds", ["0", "1", "2", "3"])
+def test_lds_modes_agree_c2(lds, monkeypatch):
+    """Every traversal mode of k_bdpt_sample on C2's scene (the bench default runs LM 3, the flat
+    leaf list, for scenes of <= 24 primitives) vs the oracle."""
+    monkeypatch.setenv("BDPT_LDS_MODE", lds)
+    W, H, S, M = 160, 120, 4, 5
+    sc = golden_scene("CBspheres", W, H)
+    g = _gpu_render(sc, W, H, S, M)
+    samp = oracle_render(sc, W, H, S, M, MODE_C32)[0]
+    assert _rmse(g["sample"], samp) < RMSE_TOL
