@@ -101,7 +101,9 @@ def test_stats_counters_match_oracle(pipe):
     assert st.closest_rays == int(o[1])
     assert st.hits == int(o[6])
     assert 0 < st.shadow_rays <= int(o[2])
-    assert 0 < st.node_visits
+    assert 0 < st.tri_tests + st.sph_tests
+    # the megakernel runs this 14-primitive scene with the flat leaf list (no node fetches)
+    assert st.node_visits > 0 or pipe == B.PIPELINE_MEGAKERNEL
 
 
 def test_trace_rays_matches_oracle():
