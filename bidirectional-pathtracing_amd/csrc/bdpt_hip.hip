@@ -504,9 +504,14 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_pt(PtKParams kp)
   const int lane = threadIdx.x & 63;
   if (LM != 0) {
     float4* sc = (float4*)smem;
-    const int nn = LM == 1 ? kp.n_node4 : node_f4(lm_width(LM)) * kp.S.ntop;
-    const int n4 = nn + (LM == 1 ? kp.n_geom4 : 0);
+    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
+    const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x) sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
+    if (LM == 3) {
+      int* lv = (int*)(sc + n4);
+      for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
+      kp.S.lleaves = lv;
+    }
     __syncthreads();
     kp.S.lnodes = sc;
     kp.S.lgeom = sc + nn;
@@ -644,12 +649,15 @@ int launch_pt(Ctx* c, PtKParams& kp) {
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const size_t lds_max = kLdsPerCu / kBlocksPerCu - 256;
   const char* env = getenv("BDPT_LDS_MODE");
-  int lm = env ? atoi(env) : (full <= lds_max ? 1 : 2);
+  const size_t flat = c->hs.geom.size() * sizeof(float) + c->hs.leaf_refs.size() * sizeof(int);
+  int lm = env ? atoi(env) : (c->hs.nprim <= kFlatMaxPrims && flat <= lds_max) ? 3 : (full <= lds_max ? 1 : 2);
+  if (lm == 3 && flat > lds_max) lm = 1;
   if (lm == 1 && full > lds_max) lm = 2;
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, lds_max / node_bytes(lm_width(2)));
+  if (lm == 3) return launch_persistent_pt(c, k_pt<STATS, 3>, flat, kp, kp.nblocks);
   if (lm == 1) return launch_persistent_pt(c, k_pt<STATS, 1>, full, kp, kp.nblocks);
   if (lm == 2) return launch_persistent_pt(c, k_pt<STATS, 2>, (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp, kp.nblocks);
   return launch_persistent_pt(c, k_pt<STATS, 0>, 0, kp, kp.nblocks);

@@ -197,7 +197,7 @@ def test_parity_env_only_scene():
 
 
 # --- the unidirectional PathTracer: k_pt vs oracle mode 2 ----------------
-@pytest.mark.parametrize("lds", ["0", "1", "2"])
+@pytest.mark.parametrize("lds", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("scene,W,H,S,M,kw", [
     ("CBspheres_lambertian", 96, 72, 8, 5, dict(samples_per_batch=4, max_tolerance=0.05)),
     ("CBspheres", 96, 72, 8, 5, dict(samples_per_batch=4, max_tolerance=0.05)),
