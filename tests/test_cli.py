@@ -68,3 +68,27 @@ def test_cli_environment_map_and_roulette(tmp_path):
     ref = read_png(tmp_path / "ref.png")
     d = np.abs(ours.astype(int) - ref.astype(int))
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
+
+
+def test_cli_pathtracer(tmp_path):
+    """--pt: the reference's unidirectional PathTracer with its -l / -a flags on a microfacet scene
+    (which BDPT rejects), against the oracle's mode 2 through the same output stage; the
+    _rate.png follows sampleCountBuffer (all pixels reach ns_aa here: tolerance 0)."""
+    import bdpt_amd as B
+    from _util import oracle_pt_render
+    W, H, S, M = 48, 36, 4, 4
+    out = tmp_path / "pt.png"
+    dae = os.path.join(REPO, "scenes", "CBspheres_microfacet_al_ag.dae")
+    r = subprocess.run([CLI, "--pt", "-s", str(S), "-m", str(M), "-l", "2", "-a", "2", "0", "-r", str(W), str(H),
+                        "-f", str(out), dae], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ours = read_png(out)
+    sc = B.load_dae(dae, W, H)
+    ref_hdr = oracle_pt_render(sc, W, H, S, M, MODE_C32, ns_area_light=2, batch=2, tol=0.0)[0]
+    raw = tmp_path / "ref.f64"
+    np.ascontiguousarray(ref_hdr, dtype="<f8").tofile(raw)
+    subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
+    ref = read_png(tmp_path / "ref.png")
+    d = np.abs(ours.astype(int) - ref.astype(int))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
+    assert np.array_equal(read_png(tmp_path / "pt_rate.png"), read_png(tmp_path / "ref_rate.png"))
