@@ -197,7 +197,7 @@ enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REF
 // Vtx::mat of a vertex without BSDF: -1 camera / area or point light vertex, MAT_ENV_V a vertex
 // of the environment light (an escaped eye ray, or an env light subpath's first vertex).
 enum { MAT_ENV_V = -2 };
-enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2 };
+enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2, LIGHT_HEMI = 3 };   // LIGHT_HEMI: PathTracer only
 // Russian roulette (bdpt_params.russian_roulette): vertices with index i > BDPT_RR_MIN continue
 // with p_keep = min(1, |f| / pdf) (the rule commented out at bidirection.cpp:87-93).
 #define BDPT_RR_MIN 3
@@ -1737,6 +1737,17 @@ BDPT_HD f3 light_sample_L(const SceneView& S, const DLight& L, Rng& g, f3 p, f3*
     *wi = normalize(d);
     *dist = norm(d);
     *pdf = 1.0f;
+    return mk3(L.rad[0], L.rad[1], L.rad[2]);
+  }
+  if (L.type == LIGHT_HEMI) {   // InfiniteHemisphereLight::sample_L (light.cpp:62-70, sampler.cpp:36-49)
+    const float Xi1 = rng_next(g);
+    const float Xi2 = rng_next(g);
+    float c, s;
+    cos_sin_2pi(Xi2, &c, &s);
+    const float st = sqrtf(fmaxf(0.0f, 1.0f - Xi1 * Xi1));   // theta = acos(Xi1)
+    *wi = mk3(st * c, Xi1, -(st * s));                        // sampleToWorld * (x, y, z) = (x, z, -y)
+    *dist = INFINITY;
+    *pdf = (float)(1.0 / (2.0 * 3.14159265358979323));   // 1 / (2 PI) in fp64, rounded once
     return mk3(L.rad[0], L.rad[1], L.rad[2]);
   }
   float sx, sy;

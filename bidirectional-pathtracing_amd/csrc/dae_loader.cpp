@@ -813,8 +813,10 @@ int load_dae(const char* path, int width, int height, DaeScene& out, std::string
       } else if (nd.lk == LK_POINT) {   // gl_scene/point_light.h:17-22
         l.type = BDPT_LIGHT_POINT;
         set3(l.position, (T * V4(nd.lpos, 1)).to3D());
+      } else if (nd.lk == LK_AMBIENT) {   // gl_scene/ambient_light.h:19-23: InfiniteHemisphereLight
+        l.type = BDPT_LIGHT_HEMISPHERE;
       } else {
-        l.type = BDPT_LIGHT_OTHER;   // ambient / directional / spot: no BDPT methods
+        l.type = BDPT_LIGHT_OTHER;   // directional / spot
       }
       out.lights.push_back(l);
     } else if (nd.type == I_SPHERE) {   // application.cpp:345-351, gl_scene/sphere.cpp:12-20
@@ -962,6 +964,9 @@ int dump_scene_json(const DaeScene& s, const char* path, std::string& err) {
     } else if (l.type == BDPT_LIGHT_POINT) {
       fprintf(f, "{\"type\": \"point\", \"radiance\": "); v3(l.radiance);
       fprintf(f, ", \"position\": "); v3(l.position);
+      fprintf(f, "}");
+    } else if (l.type == BDPT_LIGHT_HEMISPHERE) {
+      fprintf(f, "{\"type\": \"hemisphere\", \"radiance\": "); v3(l.radiance);
       fprintf(f, "}");
     } else {
       fprintf(f, "{\"type\": \"unsupported\"}");

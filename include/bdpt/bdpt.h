@@ -65,7 +65,13 @@ enum bdpt_mat_type {
 
 /* Light kinds (src/scene/light.h). Only area and point lights have BDPT methods in the reference;
  * the environment light comes in through bdpt_scene_desc.envmap, never through this list. */
-enum bdpt_light_type { BDPT_LIGHT_AREA = 0, BDPT_LIGHT_POINT = 1, BDPT_LIGHT_OTHER = 2 };
+enum bdpt_light_type {
+  BDPT_LIGHT_AREA = 0, BDPT_LIGHT_POINT = 1,
+  BDPT_LIGHT_OTHER = 2,       /* directional / spot: rejected (no BDPT methods; SpotLight::sample_L
+                                 leaves its outputs unset, light.cpp:162-165)                  */
+  BDPT_LIGHT_HEMISPHERE = 3   /* an ambient light = InfiniteHemisphereLight (light.cpp:55-65):
+                                 PathTracer only (BDPT: sample_Le asserts, :67-71)             */
+};
 
 typedef struct bdpt_material {
   int32_t type;

@@ -481,7 +481,9 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err, 
   if (d->nlight < 1 && !d->envmap) { err = "scene has no light"; return BDPT_E_INVALID; }
   for (int i = 0; i < d->nlight; i++) {
     const bdpt_light& l = d->lights[i];
-    if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT) {
+    // InfiniteHemisphereLight (light.cpp:55-98) only implements sample_L: PathTracer only
+    const bool ok = l.type == BDPT_LIGHT_AREA || l.type == BDPT_LIGHT_POINT || (pt && l.type == BDPT_LIGHT_HEMISPHERE);
+    if (!ok) {
       err = "unsupported light type under BDPT";
       return BDPT_E_UNSUPPORTED;
     }
@@ -619,6 +621,10 @@ static V3<R> env_bilerp(const EnvMap<R>& E, R x, R y) {                      // 
          (E.rgb[bottom + left] * u1 + E.rgb[bottom + right] * u0) * (1 - v1);
 }
 // xy_to_theta_phi + theta_phi_to_dir (:88-104)
+// glibc's sincos() and sin() can differ in the last bit. The compiler fuses the sin and cos of
+// theta_phi_to_dir (environment_light.cpp:110-112) into one sincos() call, but sample_L's pdf
+// (:166) calls sin() on its own: a non-inlined sin keeps that call plain here too.
+__attribute__((noinline)) static double plain_sin(double x) { return std::sin(x); }
 template <class P, class R>
 static V3<R> env_xy_to_dir(const EnvMap<R>& E, R x, R y, R* sin_theta) {
   if (P::kDevEnv) {
@@ -630,7 +636,7 @@ static V3<R> env_xy_to_dir(const EnvMap<R>& E, R x, R y, R* sin_theta) {
   }
   double phi = x / E.w * 2.0 * PI_D;
   double theta = y / E.h * PI_D;
-  *sin_theta = (R)std::sin(theta);
+  *sin_theta = (R)plain_sin(theta);   // sample_L's own sin() (:166), not the sincos() of :110-112
   return V3<R>((R)(std::cos(phi - PI_D) * std::sin(theta)), (R)std::cos(theta),
                (R)(-std::sin(phi - PI_D) * std::sin(theta)));
 }
@@ -1169,6 +1175,25 @@ struct Tracer {
       *wi = d.unit();
       *dist = d.norm();
       *pdf = 1.0;
+      return L.radiance;
+    }
+    if (L.type == BDPT_LIGHT_HEMISPHERE) {   // light.cpp:62-70 with sampler.cpp:36-49
+      R Xi1 = pol.uS();
+      R Xi2 = pol.uS();
+      V dir;
+      if (P::kDevEnv) {                       // the device's form: cos(acos x) = x, sin = sqrt(1-x^2)
+        R c, s;
+        P::cos_sin_2pi(Xi2, &c, &s);
+        const R st = std::sqrt(std::max(R(0), R(1) - Xi1 * Xi1));
+        dir = V(st * c, st * s, Xi1);
+      } else {                                // fp64 theta/phi through the float libm calls
+        const double theta = std::acos((double)Xi1);
+        const double phi = 2.0 * PI_D * (double)Xi2;
+        dir = V((R)(sinf(theta) * cosf(phi)), (R)(sinf(theta) * sinf(phi)), (R)cosf(theta));
+      }
+      *wi = V(dir.x, dir.z, -dir.y);          // sampleToWorld = [x, -z, y] columns (:55-60)
+      *dist = (R)INFINITY;
+      *pdf = R(1.0 / (2.0 * PI_D));
       return L.radiance;
     }
     R sx, sy;

@@ -51,6 +51,22 @@ def test_unsupported_material_rejected_before_device():
     assert not ctx.value
 
 
+def test_ambient_light_rejected_under_bdpt_only():
+    """An ambient light (GLScene::AmbientLight -> InfiniteHemisphereLight) only implements sample_L
+    (light.cpp:62-98): the BDPT integrator rejects it before touching a device; the PathTracer
+    accepts it (bdpt_create then fails only for want of a device here)."""
+    sc = B.load_dae(os.path.join(REPO, "scenes", "bunny.dae"), 32, 24)
+    assert [l.type for l in sc.lights] == [B.LIGHT_HEMISPHERE]
+    lib = B.load_library()
+    p = B.Params()
+    p.width, p.height, p.spp, p.max_depth = 32, 24, 1, 5
+    ctx = C.c_void_p()
+    assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) == B.BDPT_E_UNSUPPORTED
+    assert b"InfiniteHemisphereLight" in lib.bdpt_last_error()
+    p.integrator = B.INTEGRATOR_PT
+    assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) != B.BDPT_E_UNSUPPORTED
+
+
 def test_bad_frame_size_rejected():
     sc = golden_scene("CBspheres", 32, 24)
     p = B.Params()

@@ -206,6 +206,9 @@ def test_parity_env_only_scene():
     ("CBspheres_lambertian", 64, 48, 4, 4, dict(samples_per_batch=4, max_tolerance=0.05, ns_area_light=2,
                                                 direct_hemisphere_sample=True)),
     ("CBgems", 64, 48, 4, 6, dict(samples_per_batch=2, max_tolerance=0.1, lens_radius=0.05, focal_distance=4.0)),
+    # an ambient light (InfiniteHemisphereLight) on a 28k-triangle mesh, diffuse and microfacet
+    ("bunny", 64, 48, 4, 4, dict(samples_per_batch=2, max_tolerance=0.05, ns_area_light=2)),
+    ("bunny_microfacet_cu", 64, 48, 2, 3, dict(samples_per_batch=2, max_tolerance=0.05)),
 ])
 def test_pathtracer_parity_vs_oracle(scene, W, H, S, M, kw, lds, monkeypatch):
     import os

@@ -30,6 +30,9 @@ CONFIGS = {
     "env_lens": ("CBspheres_lambertian", 48, 36, 4, 4, dict(batch=4, tol=0.05, env=True, lens=0.05, focal=4.0)),
     "adaptive": ("CBempty", 48, 36, 32, 5, dict(batch=8, tol=0.1)),
     "bunny_microfacet": ("CBbunny_microfacet_cu", 48, 36, 2, 4, dict(batch=2, tol=0.05)),
+    # an ambient light (GLScene::AmbientLight -> InfiniteHemisphereLight, light.cpp:55-70)
+    "ambient": ("bunny", 48, 36, 2, 3, dict(batch=2, tol=0.05, nal=2)),
+    "ambient_microfacet_env": ("bunny_microfacet_cu", 48, 36, 2, 3, dict(batch=2, tol=0.05, env=True)),
 }
 
 
