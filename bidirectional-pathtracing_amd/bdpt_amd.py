@@ -28,7 +28,7 @@ BDPT_E_NOMEM = -4
 
 PRIM_TRIANGLE, PRIM_SPHERE = 0, 1
 MAT_DIFFUSE, MAT_EMISSION, MAT_MIRROR, MAT_GLASS, MAT_REFRACTION, MAT_MICROFACET = range(6)
-LIGHT_AREA, LIGHT_POINT, LIGHT_OTHER, LIGHT_HEMISPHERE = 0, 1, 2, 3
+LIGHT_AREA, LIGHT_POINT, LIGHT_OTHER, LIGHT_HEMISPHERE, LIGHT_DIRECTIONAL = 0, 1, 2, 3, 4
 FRAME_SAMPLE, FRAME_EYE, FRAME_LIGHT = 0, 1, 2
 
 _MAT_NAMES = {"diffuse": MAT_DIFFUSE, "emission": MAT_EMISSION, "mirror": MAT_MIRROR,
@@ -210,6 +210,9 @@ def scene_from_json(js) -> Scene:
         elif l["type"] == "hemisphere":          # an ambient light (InfiniteHemisphereLight)
             L.type = LIGHT_HEMISPHERE
             L.radiance[:] = l["radiance"]
+        elif l["type"] == "directional":         # DirectionalLight: direction = dirToLight
+            L.type = LIGHT_DIRECTIONAL
+            L.radiance[:], L.direction[:] = l["radiance"], l["direction"]
         else:
             L.type = LIGHT_OTHER
         lights.append(L)

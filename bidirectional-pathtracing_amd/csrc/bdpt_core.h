@@ -197,7 +197,7 @@ enum { MAT_DIFFUSE = 0, MAT_EMISSION = 1, MAT_MIRROR = 2, MAT_GLASS = 3, MAT_REF
 // Vtx::mat of a vertex without BSDF: -1 camera / area or point light vertex, MAT_ENV_V a vertex
 // of the environment light (an escaped eye ray, or an env light subpath's first vertex).
 enum { MAT_ENV_V = -2 };
-enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2, LIGHT_HEMI = 3 };   // LIGHT_HEMI: PathTracer only
+enum { LIGHT_AREA = 0, LIGHT_POINT = 1, LIGHT_ENV = 2, LIGHT_HEMI = 3, LIGHT_DIR = 4 };   // HEMI, DIR: PathTracer only
 // Russian roulette (bdpt_params.russian_roulette): vertices with index i > BDPT_RR_MIN continue
 // with p_keep = min(1, |f| / pdf) (the rule commented out at bidirection.cpp:87-93).
 #define BDPT_RR_MIN 3
@@ -1739,6 +1739,12 @@ BDPT_HD f3 light_sample_L(const SceneView& S, const DLight& L, Rng& g, f3 p, f3*
     *pdf = 1.0f;
     return mk3(L.rad[0], L.rad[1], L.rad[2]);
   }
+  if (L.type == LIGHT_DIR) {    // DirectionalLight::sample_L (light.cpp:17-23)
+    *wi = mk3(L.dir[0], L.dir[1], L.dir[2]);
+    *dist = INFINITY;
+    *pdf = 1.0f;
+    return mk3(L.rad[0], L.rad[1], L.rad[2]);
+  }
   if (L.type == LIGHT_HEMI) {   // InfiniteHemisphereLight::sample_L (light.cpp:62-70, sampler.cpp:36-49)
     const float Xi1 = rng_next(g);
     const float Xi2 = rng_next(g);
@@ -1790,7 +1796,7 @@ BDPT_HD f3 pt_direct(const SceneView& S, const PtParams& pp, Rng& g, const Frame
   }
   for (int l = 0; l < S.nlights; l++) {
     const DLight& L = S.lights[l];
-    const int ns = L.type == LIGHT_POINT ? 1 : pp.ns_area_light;
+    const int ns = (L.type == LIGHT_POINT || L.type == LIGHT_DIR) ? 1 : pp.ns_area_light;   // is_delta_light
     f3 L_o = splat3(0);
     for (int i = 0; i < ns; i++) {
       f3 wiw;

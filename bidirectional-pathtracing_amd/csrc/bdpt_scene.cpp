@@ -246,12 +246,13 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
   out.lights.clear();
   for (int i = 0; i < d->nlight; i++) {
     const bdpt_light& l = d->lights[i];
-    if (l.type == BDPT_LIGHT_HEMISPHERE && !pt) {
-      err = "an ambient light (InfiniteHemisphereLight) only implements sample_L: the BDPT light API asserts "
-            "(light.cpp:72-98); use the PathTracer integrator";
+    if ((l.type == BDPT_LIGHT_HEMISPHERE || l.type == BDPT_LIGHT_DIRECTIONAL) && !pt) {
+      err = "ambient (InfiniteHemisphereLight) and directional lights only implement sample_L: the BDPT light "
+            "API asserts (light.cpp:25-51,72-98); use the PathTracer integrator";
       return BDPT_E_UNSUPPORTED;
     }
-    if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT && l.type != BDPT_LIGHT_HEMISPHERE) {
+    if (l.type != BDPT_LIGHT_AREA && l.type != BDPT_LIGHT_POINT && l.type != BDPT_LIGHT_HEMISPHERE &&
+        l.type != BDPT_LIGHT_DIRECTIONAL) {
       err = "only area and point lights implement the BDPT light API (light.cpp:25-51,168-194,299-364)";
       return BDPT_E_UNSUPPORTED;
     }

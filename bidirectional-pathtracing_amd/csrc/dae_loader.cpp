@@ -815,8 +815,17 @@ int load_dae(const char* path, int width, int height, DaeScene& out, std::string
         set3(l.position, (T * V4(nd.lpos, 1)).to3D());
       } else if (nd.lk == LK_AMBIENT) {   // gl_scene/ambient_light.h:19-23: InfiniteHemisphereLight
         l.type = BDPT_LIGHT_HEMISPHERE;
+      } else if (nd.lk == LK_DIRECTIONAL) {
+        // gl_scene/directional_light.h:14-19 (a w = 1 transform of the COLLADA direction, negated,
+        // normalised), then DirectionalLight's dirToLight = -direction.unit() (light.cpp:11-15)
+        V3 d = (T * V4(nd.ldir, 1)).to3D();
+        d = V3(-d.x, -d.y, -d.z);
+        d.normalize();
+        const V3 u = d.unit();
+        l.type = BDPT_LIGHT_DIRECTIONAL;
+        set3(l.direction, V3(-u.x, -u.y, -u.z));
       } else {
-        l.type = BDPT_LIGHT_OTHER;   // directional / spot
+        l.type = BDPT_LIGHT_OTHER;   // spot
       }
       out.lights.push_back(l);
     } else if (nd.type == I_SPHERE) {   // application.cpp:345-351, gl_scene/sphere.cpp:12-20
@@ -967,6 +976,10 @@ int dump_scene_json(const DaeScene& s, const char* path, std::string& err) {
       fprintf(f, "}");
     } else if (l.type == BDPT_LIGHT_HEMISPHERE) {
       fprintf(f, "{\"type\": \"hemisphere\", \"radiance\": "); v3(l.radiance);
+      fprintf(f, "}");
+    } else if (l.type == BDPT_LIGHT_DIRECTIONAL) {
+      fprintf(f, "{\"type\": \"directional\", \"radiance\": "); v3(l.radiance);
+      fprintf(f, ", \"direction\": "); v3(l.direction);
       fprintf(f, "}");
     } else {
       fprintf(f, "{\"type\": \"unsupported\"}");

@@ -67,10 +67,12 @@ enum bdpt_mat_type {
  * the environment light comes in through bdpt_scene_desc.envmap, never through this list. */
 enum bdpt_light_type {
   BDPT_LIGHT_AREA = 0, BDPT_LIGHT_POINT = 1,
-  BDPT_LIGHT_OTHER = 2,       /* directional / spot: rejected (no BDPT methods; SpotLight::sample_L
-                                 leaves its outputs unset, light.cpp:162-165)                  */
-  BDPT_LIGHT_HEMISPHERE = 3   /* an ambient light = InfiniteHemisphereLight (light.cpp:55-65):
-                                 PathTracer only (BDPT: sample_Le asserts, :67-71)             */
+  BDPT_LIGHT_OTHER = 2,       /* spot: rejected (SpotLight::sample_L leaves its outputs unset,
+                                 light.cpp:163-166)                                            */
+  BDPT_LIGHT_HEMISPHERE = 3,  /* an ambient light = InfiniteHemisphereLight (light.cpp:55-70):
+                                 PathTracer only (BDPT: sample_Le asserts, :72-77)             */
+  BDPT_LIGHT_DIRECTIONAL = 4  /* DirectionalLight (light.cpp:11-23): `direction` = dirToLight, the
+                                 unit world direction towards the light; PathTracer only        */
 };
 
 typedef struct bdpt_material {

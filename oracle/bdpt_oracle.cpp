@@ -482,7 +482,8 @@ static int load_scene(const bdpt_scene_desc* d, Scene<R>& sc, std::string& err, 
   for (int i = 0; i < d->nlight; i++) {
     const bdpt_light& l = d->lights[i];
     // InfiniteHemisphereLight (light.cpp:55-98) only implements sample_L: PathTracer only
-    const bool ok = l.type == BDPT_LIGHT_AREA || l.type == BDPT_LIGHT_POINT || (pt && l.type == BDPT_LIGHT_HEMISPHERE);
+    const bool ok = l.type == BDPT_LIGHT_AREA || l.type == BDPT_LIGHT_POINT ||
+                    (pt && (l.type == BDPT_LIGHT_HEMISPHERE || l.type == BDPT_LIGHT_DIRECTIONAL));
     if (!ok) {
       err = "unsupported light type under BDPT";
       return BDPT_E_UNSUPPORTED;
@@ -1177,6 +1178,12 @@ struct Tracer {
       *pdf = 1.0;
       return L.radiance;
     }
+    if (L.type == BDPT_LIGHT_DIRECTIONAL) {  // light.cpp:17-23
+      *wi = L.direction;
+      *dist = (R)INFINITY;
+      *pdf = 1.0;
+      return L.radiance;
+    }
     if (L.type == BDPT_LIGHT_HEMISPHERE) {   // light.cpp:62-70 with sampler.cpp:36-49
       R Xi1 = pol.uS();
       R Xi2 = pol.uS();
@@ -1209,7 +1216,9 @@ struct Tracer {
     *pdf = sqDist / (L.area * std::fabs(cosTheta));
     return cosTheta < 0 ? L.radiance : V();
   }
-  bool light_is_delta(const Light<R>& L) const { return L.type == BDPT_LIGHT_POINT; }
+  bool light_is_delta(const Light<R>& L) const {
+    return L.type == BDPT_LIGHT_POINT || L.type == BDPT_LIGHT_DIRECTIONAL;
+  }
 
   // ---------------- camera (camera.cpp) ----------------
   Ray<R> generate_ray(R x, R y) const {                                       // :191-212

@@ -181,6 +181,11 @@ static void dump_scene(const std::string& path, RaytracedRenderer* rr, Camera& c
         << ", \"dim_y\": " << v3(a->dim_y) << ", \"area\": " << d1(a->area) << "}";
     } else if (auto* pl = dynamic_cast<SceneObjects::PointLight*>(l)) {
       o << "  {\"type\": \"point\", \"radiance\": " << v3(pl->radiance) << ", \"position\": " << v3(pl->position) << "}";
+    } else if (auto* hl = dynamic_cast<SceneObjects::InfiniteHemisphereLight*>(l)) {
+      o << "  {\"type\": \"hemisphere\", \"radiance\": " << v3(hl->radiance) << "}";
+    } else if (auto* dl = dynamic_cast<SceneObjects::DirectionalLight*>(l)) {
+      o << "  {\"type\": \"directional\", \"radiance\": " << v3(dl->radiance) << ", \"direction\": "
+        << v3(dl->dirToLight) << "}";
     } else {
       o << "  {\"type\": \"unsupported\"}";
     }

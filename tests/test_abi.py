@@ -65,6 +65,10 @@ def test_ambient_light_rejected_under_bdpt_only():
     assert b"InfiniteHemisphereLight" in lib.bdpt_last_error()
     p.integrator = B.INTEGRATOR_PT
     assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) != B.BDPT_E_UNSUPPORTED
+    sc = B.load_dae(os.path.join(REPO, "scenes", "teapot.dae"), 32, 24)   # DirectionalLight
+    assert [l.type for l in sc.lights] == [B.LIGHT_DIRECTIONAL]
+    p.integrator = B.INTEGRATOR_BDPT
+    assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) == B.BDPT_E_UNSUPPORTED
 
 
 def test_bad_frame_size_rejected():

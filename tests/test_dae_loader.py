@@ -3,6 +3,7 @@ dumps in tests/golden/scenes/*.json were written by oracle/_ref/ref_driver (Coll
 Application::load of the reference) from the same .dae files; every camera, light, material,
 sphere and triangle (positions and the halfedge-mesh vertex normals) must match bit for bit.
 CPU only (no device call)."""
+import hashlib
 import json
 import os
 
@@ -27,6 +28,25 @@ def test_loader_bit_exact_vs_reference_loader(name, tmp_path):
         got = json.load(f)
     for k in ("lights", "materials", "prim_order", "spheres", "triangles"):
         assert got[k] == ref[k], k
+    for k, v in cam.items():
+        assert got["camera"][k] == v, k
+
+
+@pytest.mark.parametrize("name", ["banana", "teapot"])
+def test_loader_directional_scenes_vs_reference_loader(name, tmp_path):
+    """dae/keenan/banana.dae (ambient + directional) and dae/meshedit/teapot.dae (directional): the
+    reference dump's lights / materials / camera verbatim, the geometry by sha256 (fixtures from
+    tools/make_pt_golden.py)."""
+    with open(os.path.join(GOLD, "scenes", name + ".compact.json")) as f:
+        ref = json.load(f)
+    cam = ref["camera"]
+    out = tmp_path / f"{name}.json"
+    B.load_dae(os.path.join(SCENES, name + ".dae"), cam["screenW"], cam["screenH"], dump_json=str(out))
+    with open(out) as f:
+        got = json.load(f)
+    assert got["lights"] == ref["lights"] and got["materials"] == ref["materials"]
+    for k in ("prim_order", "spheres", "triangles"):
+        assert hashlib.sha256(json.dumps(got[k], sort_keys=True).encode()).hexdigest() == ref[k + "_sha256"], k
     for k, v in cam.items():
         assert got["camera"][k] == v, k
 

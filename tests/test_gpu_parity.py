@@ -209,6 +209,9 @@ def test_parity_env_only_scene():
     # an ambient light (InfiniteHemisphereLight) on a 28k-triangle mesh, diffuse and microfacet
     ("bunny", 64, 48, 4, 4, dict(samples_per_batch=2, max_tolerance=0.05, ns_area_light=2)),
     ("bunny_microfacet_cu", 64, 48, 2, 3, dict(samples_per_batch=2, max_tolerance=0.05)),
+    # DirectionalLight (+ ambient on banana)
+    ("banana", 64, 48, 2, 3, dict(samples_per_batch=2, max_tolerance=0.05, ns_area_light=2)),
+    ("teapot", 64, 48, 4, 4, dict(samples_per_batch=4, max_tolerance=0.05)),
 ])
 def test_pathtracer_parity_vs_oracle(scene, W, H, S, M, kw, lds, monkeypatch):
     import os

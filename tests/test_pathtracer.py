@@ -4,7 +4,7 @@
     against the reference's own PathTracer (oracle/_ref/ref_driver -U; fixtures from
     tools/make_pt_golden.py): sampleBuffer and sampleCountBuffer (adaptive sampling), with
     MicrofacetBSDF, delta BSDFs, roulette (-m 0), hemisphere sampling (-H, -l 2), the thin lens
-    (-b, -d), the environment light and the ambient (InfiniteHemisphereLight) light;
+    (-b, -d), the environment light, ambient (InfiniteHemisphereLight) and directional lights;
   * the device code (bdpt_core.h pt_pixel, compiled for the CPU) is bit-exact against oracle
     mode 2 (fp32 device semantics, counter RNG) on the same configurations.
 The GPU kernel is checked against mode 2 in tests/test_gpu_parity.py.
@@ -20,7 +20,7 @@ from _util import MODE_C32, MODE_REF, REPO, oracle_pt_render
 
 PT = os.path.join(REPO, "tests", "golden", "pt")
 NAMES = ["lambertian", "delta", "microfacet", "roulette", "hemisphere", "env_lens", "adaptive",
-         "bunny_microfacet", "ambient", "ambient_microfacet_env"]
+         "bunny_microfacet", "ambient", "ambient_microfacet_env", "directional_ambient", "directional"]
 
 
 def _load(name):

@@ -4,10 +4,14 @@ which the reference builds but never instantiates, raytraced_renderer.cpp:53) re
 oracle/_ref/ref_driver -U at -t 1 (bit-deterministic), for SURVEY.md §8 row f4:
   <cfg>.npz : sampleBuffer (fp64, row 0 = bottom), sampleCountBuffer (int32) and the settings;
   tests/golden/scenes/CBspheres_microfacet_al_ag.json : the reference loader's dump of the
-    microfacet scene (MicrofacetBSDF eta / k / alpha).
+    microfacet scene (MicrofacetBSDF eta / k / alpha);
+  tests/golden/scenes/{banana,teapot}.compact.json : the loader dumps of the directional-light scenes
+    (geometry as sha256 of its canonical JSON).
 Run in this container (needs /root/reference and `make -f oracle/ref.mk`).
 usage: python tools/make_pt_golden.py
 """
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -33,7 +37,19 @@ CONFIGS = {
     # an ambient light (GLScene::AmbientLight -> InfiniteHemisphereLight, light.cpp:55-70)
     "ambient": ("bunny", 48, 36, 2, 3, dict(batch=2, tol=0.05, nal=2)),
     "ambient_microfacet_env": ("bunny_microfacet_cu", 48, 36, 2, 3, dict(batch=2, tol=0.05, env=True)),
+    # DirectionalLight (light.cpp:11-23): dae/keenan/banana.dae (+ ambient), dae/meshedit/teapot.dae
+    "directional_ambient": ("banana", 48, 36, 2, 3, dict(batch=2, tol=0.05, nal=2)),
+    "directional": ("teapot", 48, 36, 4, 4, dict(batch=4, tol=0.05)),
 }
+# loader dumps too large to keep whole: lights, materials and camera verbatim, the geometry hashed
+COMPACT_DUMPS = ["banana", "teapot"]
+
+
+def compact_dump(js):
+    out = {k: js[k] for k in ("lights", "materials", "camera")}
+    for k in ("prim_order", "spheres", "triangles"):
+        out[k + "_sha256"] = hashlib.sha256(json.dumps(js[k], sort_keys=True).encode()).hexdigest()
+    return out
 
 
 def main():
@@ -43,6 +59,14 @@ def main():
                         os.path.join(REPO, "tests", "golden", "scenes", "CBspheres_microfacet_al_ag.json"),
                         os.path.join(REPO, "scenes", "CBspheres_microfacet_al_ag.dae")], cwd=tmp, check=True,
                        stdout=subprocess.DEVNULL)
+        for name in COMPACT_DUMPS:
+            js = os.path.join(tmp, name + ".json")
+            subprocess.run([DRV, "-n", "-r", "800", "600", "-j", js, os.path.join(REPO, "scenes", name + ".dae")],
+                           cwd=tmp, check=True, stdout=subprocess.DEVNULL)
+            with open(js) as f:
+                dump = compact_dump(json.load(f))
+            with open(os.path.join(REPO, "tests", "golden", "scenes", name + ".compact.json"), "w") as f:
+                json.dump(dump, f, indent=1)
         for name, (scene, W, H, spp, M, st) in CONFIGS.items():
             pre = os.path.join(tmp, name)
             cmd = [DRV, "-U", "-t", "1", "-s", str(spp), "-m", str(M), "-r", str(W), str(H),
