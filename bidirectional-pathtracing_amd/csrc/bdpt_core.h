@@ -1560,10 +1560,11 @@ struct Conn {
 // A vertex that can receive a connection: diffuse (f != 0 only for DiffuseBSDF, bsdf.cpp:52-62),
 // viewed from its front side (wo.z >= 0) and carrying throughput.
 BDPT_HD bool can_connect(const Vtx& v) { return v.cq > 0.0f; }
-// ev_pre: E[i] already loaded by the caller (the megakernel's j loop reuses it), or null.
+// ev_pre / lv_pre: E[i] / L[j] already loaded by the caller (kept across the megakernel's inner
+// connection loop), or null.
 template <bool EXT = false, class PA>
 BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn,
-                      const Vtx* ev_pre = nullptr) {
+                      const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   const bool eye_cam = i == 1;
   Vtx ev, lv;
@@ -1604,7 +1605,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
   }
   // Zero-contribution connections (f_eye = 0 or f_light = 0 or zero throughput) end here.
   if (!eye_cam && !can_connect(ev)) return CONN_NONE;
-  lv = P.l(j);   // j == 1: the original L[1] (MIS quirk); j >= 2: the light endpoint
+  lv = lv_pre ? *lv_pre : P.l(j);   // j == 1: the original L[1] (MIS quirk); j >= 2: the light endpoint
   if (j >= 2 && !can_connect(lv)) return CONN_NONE;
   f3 vl_pos, vl_n, la;
   if (j == 1) {   // fresh light sample (bidirection.cpp:332-358)

@@ -252,6 +252,11 @@ constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
 #ifndef BDPT_CONN_COMPACT
 #define BDPT_CONN_COMPACT 0
 #endif
+// Connection loop order: 0 = the reference's (i outer, j inner), vertices reloaded per pair;
+// 1 = i outer with E[i] held across j; 2 = j outer with L[j] held across i.
+#ifndef BDPT_CONN_ORDER
+#define BDPT_CONN_ORDER 0
+#endif
 // Materials and lights copied to LDS (static arrays) when they fit: per-lane material / light
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
 #ifndef BDPT_MATS_LDS
@@ -369,11 +374,11 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   #endif
       // one (i, j) connection per lane (active lanes only), its ray pushed into the wave's ring,
       // the ring flushed whenever 64 rays are queued
-      auto conn_step = [&](int i, int j, bool active) {
+      auto conn_step = [&](int i, int j, bool active, const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr) {
         int kind = CONN_NONE;
         Conn cn;
         if (active) {
-          kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn);
+          kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn, ev_pre, lv_pre);
           if (kind == CONN_DIRECT) {
             dxs += cn.val.x * inv;
             dys += cn.val.y * inv;
@@ -435,6 +440,19 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
           jm &= jm - 1;
           if (jm == 0) { mE &= mE - 1; jm = mL; }
         }
+      }
+#elif BDPT_CONN_ORDER == 1
+      // E[i] loaded once per i and kept in registers across the j loop
+      for (int i = 1; i < wE; i++) {
+        const Vtx ev = P.E[i >= 2 ? i - 2 : 0];
+        for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL, i >= 2 ? &ev : nullptr);
+      }
+#elif BDPT_CONN_ORDER == 2
+      // j outer: L[j] loaded once per j and kept in registers across the i loop (the connections
+      // are order-free: per-connection RNG sub-streams, sums are fp32 atomics anyway)
+      for (int j = 0; j < wL; j++) {
+        const Vtx lv = P.L[j >= 1 ? j - 1 : 0];
+        for (int i = 1; i < wE; i++) conn_step(i, j, i < nE && j < nL, nullptr, j >= 1 ? &lv : nullptr);
       }
 #else
       for (int i = 1; i < wE; i++)
