@@ -281,7 +281,8 @@ def main() -> int:
                                f"{' + env ' + env_desc if env_desc else ''}{' RR on' if args.rr else ''}"
                                f"{' unidirectional PathTracer' if use_pt else ''}"
                                f"{' (BASELINE configs[1])' if default_workload else ''} "
-                               f"per GPU, sample-range shards + RCCL sum-reduce",
+                               + ("for the whole frame, row bands per GPU + RCCL sum-reduce" if use_pt else
+                                  "per GPU, sample-range shards + RCCL sum-reduce"),
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
                    "scene": args.scene, "width": W, "height": H, "spp_per_gpu": SPP,
                    "max_depth": M, "envmap": env_desc, "russian_roulette": args.rr,
