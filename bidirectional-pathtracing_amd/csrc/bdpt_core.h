@@ -254,6 +254,8 @@ struct SceneView {
   const float4* lgeom;   // LDS copy of the geometry (LM 1 and 3)
   const int* lleaves;    // LM 3: every leaf reference (LDS), nleaves of them
   int nleaves;
+  int fn;                // LM 3: > 0 when the leaves hold primitives 0 .. fn-1 in order (flat_prims)
+  uint32_t fsph;         // LM 3: sphere mask of those primitives
   int ntop;
   DCam cam;
   EnvView env;
@@ -371,6 +373,10 @@ namespace bdpt {
 #endif
 static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
               "BVH widths must be 2 or 4");
+// LM 3: walk the flat list as one run of primitives with the next record prefetched (S.fn > 0)
+#ifndef BDPT_FLAT_PREFETCH
+#define BDPT_FLAT_PREFETCH 1
+#endif
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
@@ -614,6 +620,34 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   int ref = S.root;
   c.closest++;
   int li = 0;
+#if BDPT_FLAT_PREFETCH
+  if (LM == 3 && S.fn > 0) {
+    // the flat list as one run of primitives, the next record's loads issued before this test
+    float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
+    for (int pi = 0; pi < S.fn; pi++) {
+      const float4 g0 = a0, g1 = a1, g2 = a2;
+      const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
+      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+      float t, b1 = 0, b2 = 0;
+      bool ok;
+      int key;
+      if ((S.fsph >> pi) & 1u) {
+        c.sphs++;
+        ok = sph_test(g0, o, d, tmin, h.t, &t);
+        key = __float_as_int(g1.x);
+      } else {
+        c.tris++;
+        ok = tri_test(g0, g1, g2, o, d, tmin, h.t, &t, &b1, &b2);
+        key = __float_as_int(g2.y);
+      }
+      if (ok && (t < h.t || key > h.key)) {
+        h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
+      }
+    }
+    if (h.prim >= 0) c.hits++;
+    return h.prim >= 0;
+  }
+#endif
   for (;;) {
     if (LM == 3) {
       if (li >= S.nleaves) break;
@@ -658,6 +692,27 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   int ref = S.root;
   c.shadow++;
   int li = 0;
+#if BDPT_FLAT_PREFETCH
+  if (LM == 3 && S.fn > 0) {
+    float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
+    for (int pi = 0; pi < S.fn; pi++) {
+      const float4 g0 = a0, g1 = a1, g2 = a2;
+      const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
+      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+      float t, b1, b2;
+      bool ok;
+      if ((S.fsph >> pi) & 1u) {
+        c.sphs++;
+        ok = sph_test(g0, o, d, tmin, tmax, &t);
+      } else {
+        c.tris++;
+        ok = tri_test(g0, g1, g2, o, d, tmin, tmax, &t, &b1, &b2);
+      }
+      if (ok) return true;
+    }
+    return false;
+  }
+#endif
   for (;;) {
     if (LM == 3) {
       if (li >= S.nleaves) return false;

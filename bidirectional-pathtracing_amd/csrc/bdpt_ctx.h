@@ -77,6 +77,7 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.lgeom = nullptr;
   S.lleaves = c->d_leaves;
   S.nleaves = (int)c->hs.leaf_refs.size();
+  S.fn = flat_prims(c->hs, &S.fsph);
   S.ntop = 0;
   S.cam = c->hs.cam;
   const HostScene& hs = c->hs;

@@ -55,6 +55,22 @@ struct HostScene {
 
 constexpr int kTopNodes = 1024;
 
+// LM 3's flat list as one run of primitives: when the device tree's leaves, in DFS order, hold
+// primitives 0, 1, ..., n-1 consecutively (the builder emits them so), returns n and sets *sph to
+// the sphere mask of those n (n <= 32); else 0 (the kernels then walk the leaf list).
+inline int flat_prims(const HostScene& hs, uint32_t* sph) {
+  *sph = 0;
+  int next = 0;
+  for (int32_t r : hs.leaf_refs) {
+    const uint32_t u = ~(uint32_t)r;
+    const int st = (int)(u >> 7), cnt = (int)(u & 7u), m = (int)((u >> 3) & 15u);
+    if (st != next || next + cnt > 32) return 0;
+    *sph |= (uint32_t)m << st;
+    next += cnt;
+  }
+  return next;
+}
+
 // Returns BDPT_OK or an error code; err receives a message.
 // pt: the scene is for the unidirectional PathTracer (microfacet materials allowed).
 int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err, bool pt = false);

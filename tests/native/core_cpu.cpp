@@ -35,6 +35,7 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.lgeom = LM == 1 || LM == 3 ? S.geom : nullptr;
   S.lleaves = hs.leaf_refs.data();
   S.nleaves = (int)hs.leaf_refs.size();
+  S.fn = flat_prims(hs, &S.fsph);
   S.ntop = 0;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
@@ -138,6 +139,8 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
   S.lgeom = nullptr;
   S.lleaves = nullptr;
   S.nleaves = 0;
+  S.fn = 0;
+  S.fsph = 0;
   S.ntop = 0;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
