@@ -377,6 +377,13 @@ static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDT
 #ifndef BDPT_FLAT_PREFETCH
 #define BDPT_FLAT_PREFETCH 1
 #endif
+// BVH leaves: the next primitive's record loaded before the current one is tested, where the
+// geometry comes from HBM (LM 0 / 2). Measured: Lucy stand-in 1080p 489 -> 516, CBbunny 800x600
+// 351 -> 370 Msamples/s; with the geometry in LDS (LM 1, CBgems) 303 -> 299, so off there.
+#ifndef BDPT_LEAF_PREFETCH
+#define BDPT_LEAF_PREFETCH 1
+#endif
+BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM == 0 || LM == 2); }
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
@@ -656,20 +663,40 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
     if (ref == kTravDone) break;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+    float4 a0, a1, a2;
+    if constexpr (leaf_prefetch(LM)) {
+      a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
+    }
     for (int k = 0; k < cnt; k++) {
       const int pi = st + k;
       float t, b1 = 0, b2 = 0;
       bool ok;
       int key;
-      if ((sm >> k) & 1) {
-        c.sphs++;
-        ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
-        key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
+      if constexpr (leaf_prefetch(LM)) {
+        // this record was loaded one test ahead; issue the next one's loads before testing it
+        const float4 g0 = a0, g1 = a1, g2 = a2;
+        const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
+        a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(g0, o, d, tmin, h.t, &t);
+          key = __float_as_int(g1.x);
+        } else {
+          c.tris++;
+          ok = tri_test(g0, g1, g2, o, d, tmin, h.t, &t, &b1, &b2);
+          key = __float_as_int(g2.y);
+        }
       } else {
-        c.tris++;
-        const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
-        ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
-        key = __float_as_int(g2.y);
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
+          key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
+        } else {
+          c.tris++;
+          const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
+          ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
+          key = __float_as_int(g2.y);
+        }
       }
       // t <= h.t here; an equal t replaces the hit only if it comes later in the reference's DFS
       // leaf order (the reference keeps the last of equal-t hits)
@@ -721,16 +748,33 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+    float4 a0, a1, a2;
+    if constexpr (leaf_prefetch(LM)) {
+      a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
+    }
     for (int k = 0; k < cnt; k++) {
       const int pi = st + k;
       float t, b1, b2;
       bool ok;
-      if ((sm >> k) & 1) {
-        c.sphs++;
-        ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, tmax, &t);
+      if constexpr (leaf_prefetch(LM)) {
+        const float4 g0 = a0, g1 = a1, g2 = a2;
+        const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
+        a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(g0, o, d, tmin, tmax, &t);
+        } else {
+          c.tris++;
+          ok = tri_test(g0, g1, g2, o, d, tmin, tmax, &t, &b1, &b2);
+        }
       } else {
-        c.tris++;
-        ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), ld_geom<LM>(S, 3 * pi + 2), o, d, tmin, tmax, &t, &b1, &b2);
+        if ((sm >> k) & 1) {
+          c.sphs++;
+          ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, tmax, &t);
+        } else {
+          c.tris++;
+          ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), ld_geom<LM>(S, 3 * pi + 2), o, d, tmin, tmax, &t, &b1, &b2);
+        }
       }
       if (ok) return true;
     }
