@@ -252,6 +252,7 @@ struct SceneView {
   int root;              // root child reference
   const float4* lnodes;  // LDS copy of nodes [0, ntop) (LM 1: all nodes; LM 2: BFS treelet)
   const float4* lgeom;   // LDS copy of the geometry (LM 1 and 3)
+  const float4* lshade;  // LDS copy of the shading records (LM 3)
   const int* lleaves;    // LM 3: every leaf reference (LDS), nleaves of them
   int nleaves;
   int fn;                // LM 3: > 0 when the leaves hold primitives 0 .. fn-1 in order (flat_prims)
@@ -839,12 +840,19 @@ BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmi
 
 // Shading record of a closest hit: interpolated normal (triangle.cpp:80-82) or sphere normal
 // (sphere.cpp:78-81), and the material.
+template <int LM = 0>
 BDPT_HD void shade_hit(const SceneView& S, const Hit& h, f3 o, f3 d, f3* n_out, int* mat_out) {
-  const float4* sh = S.shade + 3 * h.prim;
-  float4 s0 = ld_glb4(sh), s1 = ld_glb4(sh + 1), s2 = ld_glb4(sh + 2);
+  float4 s0, s1, s2;
+  if (LM == 3) {   // the flat list's shading records are staged in LDS with its geometry
+    const float4* sh = S.lshade + 3 * h.prim;
+    s0 = ld_lds4(sh); s1 = ld_lds4(sh + 1); s2 = ld_lds4(sh + 2);
+  } else {
+    const float4* sh = S.shade + 3 * h.prim;
+    s0 = ld_glb4(sh); s1 = ld_glb4(sh + 1); s2 = ld_glb4(sh + 2);
+  }
   *mat_out = __float_as_int(s2.y);
   if (__float_as_int(s2.z) != 0) {   // sphere: center in geom
-    float4 g = ld_glb4(S.geom + 3 * h.prim);
+    float4 g = ld_geom<LM>(S, 3 * h.prim);
     f3 p = add(o, smul(h.t, d));
     *n_out = normalize(sub(p, mk3(g.x, g.y, g.z)));
   } else {
@@ -1584,7 +1592,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     if (!end) {
       f3 n;
       int mat;
-      shade_hit(S, h, ro, rd, &n, &mat);
+      shade_hit<LM>(S, h, ro, rd, &n, &mat);
       const DMat M = S.mats[mat];
       const Frame fr = make_frame(n);
       const f3 hit_p = add(ro, muls(rd, h.t));
@@ -1888,7 +1896,7 @@ BDPT_HD f3 pt_direct(const SceneView& S, const PtParams& pp, Rng& g, const Frame
       if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h, cnt)) continue;
       f3 hn;
       int hm;
-      shade_hit(S, h, hit_p, wiw, &hn, &hm);
+      shade_hit<LM>(S, h, hit_p, wiw, &hn, &hm);
       const float ct = fabsf(dot(wiw, n));
       L_out = add(L_out, divs(muls(mul(mat_emission(S, hm), f), ct), pdf));
     }
@@ -1940,7 +1948,7 @@ BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int 
     return S.env.light >= 0 ? env_radiance(S.env, rd) : splat3(0);
   f3 n;
   int mat;
-  shade_hit(S, h, ro, rd, &n, &mat);
+  shade_hit<LM>(S, h, ro, rd, &n, &mat);
   const f3 E0 = mat_emission(S, mat);
   // forward walk: per vertex k the NEE value, and for a continued walk f, cos, pdf, the roulette
   // flag and the next hit's emission (used when vertex k is delta)
@@ -1969,7 +1977,7 @@ BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int 
     if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h2, cnt)) break;
     f3 n2;
     int m2;
-    shade_hit(S, h2, hit_p, wiw, &n2, &m2);
+    shade_hit<LM>(S, h2, hit_p, wiw, &n2, &m2);
     fk[k] = f;
     ck[k] = fabsf(dot(wiw, n));
     pk[k] = pdf;

@@ -75,6 +75,7 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.root = c->hs.tree(W).root;
   S.lnodes = nullptr;
   S.lgeom = nullptr;
+  S.lshade = nullptr;
   S.lleaves = c->d_leaves;
   S.nleaves = (int)c->hs.leaf_refs.size();
   S.fn = flat_prims(c->hs, &S.fsph);

@@ -290,6 +290,9 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       int* lv = (int*)(sc + n4);
       for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
       kp.S.lleaves = lv;
+      float4* ls = sc + n4 + (kp.S.nleaves + 3) / 4;   // shading records after the leaf list
+      for (int k = threadIdx.x; k < kp.n_geom4; k += blockDim.x) ls[k] = kp.S.shade[k];
+      kp.S.lshade = ls;
     }
     __syncthreads();
     kp.S.lnodes = sc;
@@ -529,6 +532,9 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_pt(PtKParams kp)
       int* lv = (int*)(sc + n4);
       for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
       kp.S.lleaves = lv;
+      float4* ls = sc + n4 + (kp.S.nleaves + 3) / 4;   // shading records after the leaf list
+      for (int k = threadIdx.x; k < kp.n_geom4; k += blockDim.x) ls[k] = kp.S.shade[k];
+      kp.S.lshade = ls;
     }
     __syncthreads();
     kp.S.lnodes = sc;
@@ -629,7 +635,8 @@ int launch_lm(Ctx* c, KParams& kp) {
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const bool has_nodes = !c->hs.bvh2.nodes.empty();
   const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2 / 3
-  const size_t flat = c->hs.geom.size() * sizeof(float) + c->hs.leaf_refs.size() * sizeof(int);
+  // LM 3's LDS: geometry, leaf list (padded to 16 B), shading records
+  const size_t flat = 2 * c->hs.geom.size() * sizeof(float) + (c->hs.leaf_refs.size() + 3) / 4 * 16;
   int lm = env ? atoi(env)
                : (c->hs.nprim <= kFlatMaxPrims && flat <= kLdsSceneMax) ? 3
                : (full <= kLdsSceneMax ? 1 : has_nodes ? 2 : 0);
@@ -667,7 +674,8 @@ int launch_pt(Ctx* c, PtKParams& kp) {
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const size_t lds_max = kLdsPerCu / kBlocksPerCu - 256;
   const char* env = getenv("BDPT_LDS_MODE");
-  const size_t flat = c->hs.geom.size() * sizeof(float) + c->hs.leaf_refs.size() * sizeof(int);
+  // LM 3's LDS: geometry, leaf list (padded to 16 B), shading records
+  const size_t flat = 2 * c->hs.geom.size() * sizeof(float) + (c->hs.leaf_refs.size() + 3) / 4 * 16;
   int lm = env ? atoi(env) : (c->hs.nprim <= kFlatMaxPrims && flat <= lds_max) ? 3 : (full <= lds_max ? 1 : 2);
   if (lm == 3 && flat > lds_max) lm = 1;
   if (lm == 1 && full > lds_max) lm = 2;

@@ -33,6 +33,7 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   // LM 1 reads the "LDS copy": on the CPU the same arrays (exercises the LDS-mode tree)
   S.lnodes = LM == 1 ? S.nodes : nullptr;
   S.lgeom = LM == 1 || LM == 3 ? S.geom : nullptr;
+  S.lshade = LM == 3 ? S.shade : nullptr;
   S.lleaves = hs.leaf_refs.data();
   S.nleaves = (int)hs.leaf_refs.size();
   S.fn = flat_prims(hs, &S.fsph);
@@ -137,6 +138,7 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
   S.root = T.root;
   S.lnodes = nullptr;
   S.lgeom = nullptr;
+  S.lshade = nullptr;
   S.lleaves = nullptr;
   S.nleaves = 0;
   S.fn = 0;
