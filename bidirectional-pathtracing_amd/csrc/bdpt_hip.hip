@@ -646,6 +646,7 @@ int launch_lm(Ctx* c, KParams& kp) {
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
+  if (lm == 2 && getenv("BDPT_NTOP_MAX")) kp.S.ntop = std::min(kp.S.ntop, atoi(getenv("BDPT_NTOP_MAX")));   // diagnostics
   if (lm == 3) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 3, EXT>, q + flat, kp);
   if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, q + full, kp);
   if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
