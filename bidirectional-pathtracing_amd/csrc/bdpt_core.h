@@ -1185,6 +1185,11 @@ BDPT_HD float step_gx(f3 cur_pos, f3 cur_n, bool cur_env, f3 oth_pos, f3 oth_zh,
 }
 BDPT_HD bool is_env(const Vtx& v) { return v.mat == MAT_ENV_V; }
 
+// Non-EXT walks compute each vertex's MIS constants when the vertex is created (prepare_sample);
+// the two passes below then run only for EXT kernels.
+#ifndef BDPT_FUSED_CONSTANTS
+#define BDPT_FUSED_CONSTANTS 1
+#endif
 // Per-subpath MIS constants (see Vtx). EXT: the scene has an environment light or the walks use
 // Russian roulette (q = Vtx::gp on entry); EXT = false compiles to the reference-only path.
 template <int MAXV, bool EXT = false>
@@ -1558,6 +1563,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.alpha = divs(lrad, lpp);
     v1.mat = l1env ? (int)MAT_ENV_V : -1;
     v1.gp = 0; v1.cq = 0;
+    v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused non-EXT walk)
   }
   P.l1_dir_pdf = mis_dir;
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
@@ -1604,8 +1610,30 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.mat = mat;
       v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
       Vtx* slot = (light ? P.L + 1 : P.E) + count++;
-      *slot = v;
       if (is_delta(M.type)) dm |= 1u << i;
+#if BDPT_FUSED_CONSTANTS
+      if (!EXT) {
+        // eye_constants / light_constants of this vertex at its creation: the previous vertex is the
+        // one just below it on the same subpath (camera: no step; light vertex L[1] for the light's
+        // first hit), so nothing is re-read after the walk
+        const bool conn = M.type == MAT_DIFFUSE && lz(normalize(sub(ro, v.pos)), v.zh) >= 0 && nonzero3(v.alpha);
+        v.cq = conn ? 1.0f : 0.0f;
+        if (!light && count == 1) {
+          v.fwd = 1.0f * 1.0f;
+          v.gp = 0.0f;
+        } else {
+          const Vtx nx = light ? P.L[count - 1] : P.E[count - 2];
+          f3 dw;
+          const float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
+          const float p = (light && count == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw);
+          v.fwd = p * g2;
+          const float g = step_g(nx.pos, nx.n, v.pos, v.zh, &dw);
+          const float pp = pdf_b(M, v.n, v.zh, dw);
+          v.gp = mis_horner((pp * g) / nx.fwd, !((dm >> (i - 2)) & 3u), nx.gp);
+        }
+      }
+#endif
+      *slot = v;
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
       } else {
@@ -1649,8 +1677,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       i = 2; count = 0; dm = 0;
     }
   }
-  eye_constants<MAXV, EXT>(S, P);
-  light_constants<MAXV, EXT>(S, P, mis_p);
+  if (EXT || !BDPT_FUSED_CONSTANTS) {
+    eye_constants<MAXV, EXT>(S, P);
+    light_constants<MAXV, EXT>(S, P, mis_p);
+  }
 }
 
 // What estimate_bidirection_radiance (bidirection.cpp:296-469) computes for pair (i, j) up to its

@@ -70,14 +70,16 @@ def test_cli_environment_map_and_roulette(tmp_path):
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
 
 
-def test_cli_pathtracer(tmp_path):
-    """--pt: the reference's unidirectional PathTracer with its -l / -a flags on a microfacet scene
-    (which BDPT rejects), against the oracle's mode 2 through the same output stage."""
+@pytest.mark.parametrize("scene", ["CBspheres_microfacet_al_ag", "banana"])
+def test_cli_pathtracer(tmp_path, scene):
+    """--pt: the reference's unidirectional PathTracer with its -l / -a flags on scenes BDPT rejects
+    (a microfacet scene; dae/keenan/banana.dae with its ambient and directional lights), against the
+    oracle's mode 2 through the same output stage."""
     import bdpt_amd as B
     from _util import oracle_pt_render
     W, H, S, M = 48, 36, 4, 4
     out = tmp_path / "pt.png"
-    dae = os.path.join(REPO, "scenes", "CBspheres_microfacet_al_ag.dae")
+    dae = os.path.join(REPO, "scenes", scene + ".dae")
     r = subprocess.run([CLI, "--pt", "-s", str(S), "-m", str(M), "-l", "2", "-a", "2", "0", "-r", str(W), str(H),
                         "-f", str(out), dae], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
