@@ -906,10 +906,10 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   }
   int spl = c->prm.samples_per_lane;
   if (spl <= 0) {
-    // ~16 work items per co-resident wave (dynamic balance), as few chunks as that allows
-    const long long want = 16LL * 16 * c->ncu;
-    long long nch = std::min<long long>(spp_count, std::max(1LL, (want + kp.nblocks - 1) / kp.nblocks));
-    spl = (int)((spp_count + nch - 1) / nch);
+    // small work items (8x8 pixels x 4 samples): measured against the earlier "~16 items per
+    // co-resident wave" rule (spl 6 on C2, 43 on the 1080p stand-in): C2 586 -> 586-590, Lucy
+    // stand-in 1080p 532 -> 539 Msamples/s; spl 8 / 16 / 32 lose 1-14% (tools/gpu_spl.sh)
+    spl = (int)std::min<long long>(spp_count, 4);
   }
   kp.spl = spl;
   kp.spp_begin = spp_begin;
