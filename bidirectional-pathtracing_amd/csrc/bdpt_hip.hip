@@ -41,6 +41,8 @@ struct KParams {
   int nbx;                    // full-frame: blocks per row
   int spp_begin, spp_end, spl;
   unsigned nitems;            // work items = nblocks * ceil(spp_count / spl)
+  unsigned nchunks;           // ceil(spp_count / spl)
+  int block_major;            // 1: consecutive tickets walk one pixel block's chunks
   unsigned* work;             // ticket counter (zeroed before each launch)
   int n_node4, n_geom4;       // float4 counts of the node / geometry arrays (LDS staging)
   int nmat;
@@ -329,8 +331,14 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     if (lane == 0) item = atomicAdd(kp.work, 1u);
     item = __shfl(item, 0, 64);
     if (item >= kp.nitems) break;
-    const int chunk = (int)(item / (unsigned)kp.nblocks);
-    const int blk = (int)(item - (unsigned)chunk * (unsigned)kp.nblocks);
+    int chunk, blk;
+    if (kp.block_major) {
+      blk = (int)(item / kp.nchunks);
+      chunk = (int)(item - (unsigned)blk * kp.nchunks);
+    } else {
+      chunk = (int)(item / (unsigned)kp.nblocks);
+      blk = (int)(item - (unsigned)chunk * (unsigned)kp.nblocks);
+    }
     int bx0, by0, bw, bh;
     if (kp.blocks) {
       int4 bb = kp.blocks[blk];
@@ -918,6 +926,10 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   const long long nitems = nchunks * kp.nblocks;
   if (nitems >= 0x7fffffffLL) { g_err = "launch too large; split spp"; return BDPT_E_INVALID; }
   kp.nitems = (unsigned)nitems;
+  kp.nchunks = (unsigned)nchunks;
+  // consecutive tickets take one pixel block's sample chunks in turn (measured: C2 +1.2%, CBgems
+  // +2%, Lucy stand-in 1080p +-0 over chunk-major order); BDPT_BLOCK_MAJOR=0 restores chunk-major
+  kp.block_major = getenv("BDPT_BLOCK_MAJOR") ? atoi(getenv("BDPT_BLOCK_MAJOR")) : 1;
   kp.work = (unsigned*)(c->d_stats + 15);
   HIPCHK(hipMemsetAsync(kp.work, 0, sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
