@@ -914,10 +914,11 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   }
   int spl = c->prm.samples_per_lane;
   if (spl <= 0) {
-    // small work items (8x8 pixels x 4 samples): measured against the earlier "~16 items per
-    // co-resident wave" rule (spl 6 on C2, 43 on the 1080p stand-in): C2 586 -> 586-590, Lucy
-    // stand-in 1080p 532 -> 539 Msamples/s; spl 8 / 16 / 32 lose 1-14% (tools/gpu_spl.sh)
-    spl = (int)std::min<long long>(spp_count, 4);
+    // small work items (8x8 pixels x 2 samples): measured against the earlier "~16 items per
+    // co-resident wave" rule (spl 6 on C2, 43 on the 1080p stand-in): C2 586 -> 591, Lucy stand-in
+    // 1080p 532 -> 536-539 Msamples/s; with block-major order spl 2 vs 4: CBgems 313 vs 305, C2 and
+    // the stand-in equal; spl 8 / 16 / 32 lose 1-14% (tools/gpu_spl.sh)
+    spl = (int)std::min<long long>(spp_count, 2);
   }
   kp.spl = spl;
   kp.spp_begin = spp_begin;
