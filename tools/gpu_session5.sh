@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-1 v13 session: GPU tests, smoke, the default bench under rocprofv3 stats, the north-star and
+# Round-1 v14 session: GPU tests, smoke, the default bench under rocprofv3 stats, the north-star and
 # C5 stand-ins, the PathTracer benches, then FETCH/WRITE PMC passes of one C2 launch.
 cd "$(dirname "$0")/.." || exit 1
 OUT=gpurun_out
