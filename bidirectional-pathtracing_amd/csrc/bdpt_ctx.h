@@ -38,6 +38,7 @@ struct Ctx {
   int* d_leaves = nullptr;     // HostScene::leaf_refs (LM 3 staging source)
   float* d_env = nullptr;      // HostScene::env (environment light tables + map)
   int* d_count = nullptr;      // PathTracer::sampleCountBuffer (W*H)
+  unsigned* d_work8 = nullptr;  // 8 per-XCD-group ticket counters, 128 B apart
   bool pt = false;             // bdpt_params.integrator == BDPT_INTEGRATOR_PT
   float* d_eye = nullptr;
   float* d_light = nullptr;

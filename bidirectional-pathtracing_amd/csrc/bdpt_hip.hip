@@ -44,6 +44,9 @@ struct KParams {
   unsigned nchunks;           // ceil(spp_count / spl)
   int block_major;            // 1: consecutive tickets walk one pixel block's chunks
   unsigned* work;             // ticket counter (zeroed before each launch)
+  unsigned* work8;            // XCD mode: 8 ticket counters, 128 B apart (zeroed before each launch)
+  unsigned region;            // XCD mode: items per group, ceil(nitems / 8)
+  int xcd;                    // 1: blocks b, b+8, ... (one XCD) take items from their own eighth first
   int n_node4, n_geom4;       // float4 counts of the node / geometry arrays (LDS staging)
   int nmat;
 };
@@ -326,11 +329,32 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   // global ticket counter until none are left, so per-item cost differences (path lengths, scene
   // regions) never leave CUs idle at the tail of the launch. Every wave exits at the first
   // ticket >= nitems.
+  // XCD mode: blocks b and b + 8 share an XCD (round-robin dealing, MI355X_MICROARCH.md), so group
+  // g = b % 8 works through its own contiguous eighth of the items (a contiguous band of pixel
+  // blocks, whose BVH region then stays in that XCD's L2) and only then helps the other groups.
+  const int grp = blockIdx.x & 7;
+  int cur = 0;   // wave-uniform: groups exhausted so far
   for (;;) {
     unsigned item = 0;
-    if (lane == 0) item = atomicAdd(kp.work, 1u);
-    item = __shfl(item, 0, 64);
-    if (item >= kp.nitems) break;
+    if (kp.xcd) {
+      item = 0xffffffffu;
+      if (lane == 0) {
+        for (; cur < 8; cur++) {
+          const unsigned gg = (unsigned)((grp + cur) & 7);
+          const unsigned lo = gg * kp.region;
+          if (lo >= kp.nitems) continue;
+          const unsigned t = atomicAdd(kp.work8 + 32 * gg, 1u);
+          if (t < kp.region && lo + t < kp.nitems) { item = lo + t; break; }
+        }
+      }
+      item = __shfl(item, 0, 64);
+      cur = __shfl(cur, 0, 64);
+      if (item == 0xffffffffu) break;
+    } else {
+      if (lane == 0) item = atomicAdd(kp.work, 1u);
+      item = __shfl(item, 0, 64);
+      if (item >= kp.nitems) break;
+    }
     int chunk, blk;
     if (kp.block_major) {
       blk = (int)(item / kp.nchunks);
@@ -700,7 +724,7 @@ int launch_pt(Ctx* c, PtKParams& kp) {
 
 void free_ctx(Ctx* c) {
   if (!c) return;
-  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count, c->d_leaves,
+  void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count, c->d_work8, c->d_leaves,
                   c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -784,6 +808,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if (hipMalloc((void**)&c->d_eye, fb) != hipSuccess || hipMalloc((void**)&c->d_light, fb) != hipSuccess ||
       hipMalloc((void**)&c->d_sample, fb) != hipSuccess ||
       hipMalloc((void**)&c->d_count, c->npix * sizeof(int)) != hipSuccess ||
+      hipMalloc((void**)&c->d_work8, 8 * 32 * sizeof(unsigned)) != hipSuccess ||
       hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "out of device memory";
     return fail(BDPT_E_NOMEM);
@@ -933,6 +958,10 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.block_major = getenv("BDPT_BLOCK_MAJOR") ? atoi(getenv("BDPT_BLOCK_MAJOR")) : 1;
   kp.work = (unsigned*)(c->d_stats + 15);
   HIPCHK(hipMemsetAsync(kp.work, 0, sizeof(unsigned), c->stream));
+  kp.work8 = c->d_work8;
+  kp.region = (kp.nitems + 7u) / 8u;
+  kp.xcd = getenv("BDPT_XCD_GROUPS") ? atoi(getenv("BDPT_XCD_GROUPS")) : 0;
+  if (kp.xcd) HIPCHK(hipMemsetAsync(kp.work8, 0, 8 * 32 * sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp) : launch_maxv<16>(c, kp);
   if (rc) return rc;
