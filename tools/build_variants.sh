@@ -5,8 +5,10 @@ cd "$(dirname "$0")/.." || exit 1
 CS=bidirectional-pathtracing_amd/csrc
 FL="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Iinclude -I$CS"
 mkdir -p build/var
+# a common unit is rebuilt when its source or any header (bdpt_ctx.h's Ctx layout included) is newer
+newest_h=$(ls -t $CS/*.h include/bdpt/*.h | head -1)
 for u in bdpt_wavefront.hip bdpt_scene.cpp dae_loader.cpp exr_loader.cpp; do
-  [ build/var/$u.o -nt $CS/$u ] && [ build/var/$u.o -nt $CS/bdpt_core.h ] || hipcc $FL -c $CS/$u -o build/var/$u.o &
+  [ build/var/$u.o -nt $CS/$u ] && [ build/var/$u.o -nt "$newest_h" ] || hipcc $FL -c $CS/$u -o build/var/$u.o &
 done
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
