@@ -120,6 +120,14 @@ extern "C" int core_cpu_scene_info(const bdpt_scene_desc* d, int* depth, int* re
 
 // The unidirectional PathTracer (bdpt_core.h pt_pixel) for the whole frame: image = W*H*3
 // (sampleBuffer), counts = W*H (sampleCountBuffer).
+// LDS mode 3's flat primitive run (flat_prims): its length, or 0 when the leaves are not one run
+extern "C" int core_cpu_flat_prims(const bdpt_scene_desc* d, uint32_t* sph_mask) {
+  HostScene hs;
+  std::string err;
+  if (build_host_scene(d, hs, err) != BDPT_OK) return -1;
+  return flat_prims(hs, sph_mask);
+}
+
 extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed,
                                   int ns_area_light, int batch, float tol, int hemisphere, double lens,
                                   double focal, double* image, int* counts) {
