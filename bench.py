@@ -2,19 +2,30 @@
 """Benchmark of the BDPT hot path on MI355X (BASELINE.json metric: Msamples/s at m=5, plus
 per-pixel RMSE vs the CPU path at a matched seed).
 
-Workload (N=1): BASELINE.json configs[1] — dae/sky/CBspheres.dae (mirror + glass spheres),
-480x360, 128 spp, -m 5, on one MI355X. One "step" = one full-frame render of 128 samples per
-pixel (22.1 M pixel-samples) through the C-ABI (libbdpt_amd.so, k_bdpt_sample).
-Multi-GPU (torchrun, one rank per GPU): weak scaling — rank r renders the global sample range
-[r*128, (r+1)*128) of every pixel (sample keys are global, so the image is independent of the
-rank count up to fp32 summation order) and the W*H*3 fp32 frames are summed over RCCL (xGMI)
-onto rank 0 inside the timed region. value = all ranks' samples / max-over-ranks time.
+Default workload (N=1, and the fixed render split across ranks for N>1): the north-star target,
+CBlucy 1920x1080 -s 128 -m 5. dae/sky/CBlucy.dae is absent from the reference checkout
+(.MISSING_LARGE_BLOBS), so the scene is its stand-in scenes/CBlucy_standin.dae (SURVEY.md §8d:
+CBbunny's box, light and camera, the bunny subdivided 1->4 to 114,304 triangles; written by
+tools/gen_standin.py), loaded through the product loader (bdpt_dae_load, the reference CLI's
+ColladaParser + Application::load path). One "step" = one full 1920x1080 frame of 128 samples per
+pixel (265.4 M pixel-samples) through the C-ABI (libbdpt_amd.so, k_bdpt_sample).
+Other BASELINE configs: --workload c2 | c3 | c4 | c5 (c5's ennis.exr is an LFS pointer in the
+reference: a synthetic sky of the same role stands in, tools/envmap.py).
+
+Multi-GPU (torchrun, one rank per GPU), strong scaling by default: the step's fixed render (the
+workload's spp of every pixel) is split by sample range — rank r renders global sample indices
+[s*spp + r*spp/N, s*spp + (r+1)*spp/N) of step s (sample keys are global, so the image does not
+depend on N up to fp32 summation order) — and the W*H*3 fp32 frames are summed by one RCCL reduce
+onto rank 0 inside the timed region (splats land anywhere, so a tile gather would not do,
+SURVEY.md §8e). --scaling weak gives every rank the full spp instead. value = pixel-samples of all
+ranks / max-over-ranks wall time.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -25,15 +36,29 @@ for p in (PKG, os.path.join(REPO, "tests")):
         sys.path.insert(0, p)
 
 METRIC = "Msamples/sec (spp×pixels/s) at m=5; per-pixel RMSE vs CPU at matched seed"
-SCENE, W, H, SPP, M = "CBspheres", 480, 360, 128, 5
+STANDIN = "scenes/CBlucy_standin.dae"
+# name: (scene, W, H, spp, max_depth, envmap, russian roulette, what it is)
+WORKLOADS = {
+    "ns": (STANDIN, 1920, 1080, 128, 5, None, False,
+           "north star: CBlucy (stand-in) 1920x1080 -s 128 -m 5"),
+    "c2": ("scenes/CBspheres.dae", 480, 360, 128, 5, None, False, "BASELINE configs[1]: CBspheres 480x360 -s 128 -m 5"),
+    "c3": (STANDIN, 800, 600, 128, 5, None, False, "BASELINE configs[2]: CBlucy (stand-in) 800x600 -s 128 -m 5"),
+    "c4": ("scenes/CBgems.dae", 1920, 1080, 256, 7, None, False, "BASELINE configs[3]: CBgems 1920x1080 -s 256 -m 7"),
+    "c5": (STANDIN, 1920, 1080, 1024, 8, "synth:1024x512", True,
+           "BASELINE configs[4]: CBlucy (stand-in) + env (synthetic sky for ennis.exr) 1920x1080 -s 1024 -m 8 RR"),
+}
 HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_NODE, BYTES_TRI, BYTES_SPH, BYTES_HIT = 32, 36, 16, 40
 
 
-def rank_sample_range(step: int, rank: int, world: int, spp: int):
-    """Global sample indices [begin, begin + spp) that `rank` renders in `step`: every step and
-    rank owns a fresh range, so the N-GPU image equals a single render of N*spp samples (sample
-    keys are global)."""
+def rank_sample_range(step: int, rank: int, world: int, spp: int, scaling: str = "strong"):
+    """Global sample indices [begin, begin + count) that `rank` renders in `step`.
+    strong: the step's fixed render of `spp` samples per pixel is split across the ranks;
+    weak: every rank renders a fresh `spp` of its own. Either way every (step, rank) owns a
+    disjoint range, so the summed frames equal one render of all those samples."""
+    if scaling == "strong":
+        lo, hi = spp * rank // world, spp * (rank + 1) // world
+        return step * spp + lo, hi - lo
     return (step * world + rank) * spp, spp
 
 
@@ -42,10 +67,29 @@ def algorithmic_bytes(st) -> int:
             + BYTES_HIT * st.hits)
 
 
-def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0, rr: bool = False) -> dict:
+def global_memory_bytes(st) -> int:
+    """The algorithmic bytes minus what the kernel read from the CU's LDS copy of the scene (the
+    BFS treelet in LDS mode 2; the whole scene in modes 1 / 3): the part that has to come through
+    the L2 / HBM path."""
+    lm = st.lds_mode
+    nodes = st.node_visits - st.lds_node_visits
+    prims = 0 if lm in (1, 3) else BYTES_TRI * st.tri_tests + BYTES_SPH * st.sph_tests
+    hits = 0 if lm == 3 else BYTES_HIT * st.hits
+    return BYTES_NODE * nodes + prims + hits
+
+
+def ensure_standin(path: str) -> None:
+    """scenes/CBlucy_standin.dae is generated (deterministic, 4 MB) rather than committed."""
+    if os.path.basename(path) == os.path.basename(STANDIN) and not os.path.exists(path):
+        subprocess.run([sys.executable, os.path.join(REPO, "tools", "gen_standin.py"),
+                        os.path.join(REPO, "scenes", "CBbunny.dae"), path], check=True)
+
+
+def cpu_baseline(scene, name: str, W: int, H: int, SPP: int, M: int, threads: int, budget_s: float = 12.0,
+                 rr: bool = False) -> dict:
     """The oracle's fp64 reference-semantics path (mode COUNTER64: the reference's arithmetic,
     multi-threaded like the reference's -t N) timed on this host on a bounded sample of the same
-    workload (full 480x360 frame, a few spp)."""
+    workload (full frame, a few spp)."""
     from _util import MODE_C64, oracle_render
     done, t_tot, spp_run = 0, 0.0, 1
     s0 = 0
@@ -66,14 +110,13 @@ def cpu_baseline(scene, name: str, threads: int, budget_s: float = 12.0, rr: boo
 REF_DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
 
 
-def cpu_baseline_reference(dae: str, name: str, threads: int, budget_s: float = 15.0):
+def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads: int, budget_s: float = 15.0):
     """The reference's own `-t N` CPU path: oracle/_ref/ref_driver (built by __graft_entry__.build()
     from the reference's sources: RaytracedRenderer + BidirectionalPathTracer, reference flags)
     rendering the same scene and resolution at a few spp. Render seconds are the reference's own
     "Rendering... 100%! (Xs)" report (tiles + its per-tile frame tonemap, excluding parse/BVH
     build). None when the binary is not present."""
     import re
-    import subprocess
     import tempfile
     if not os.path.exists(REF_DRIVER) or not os.path.exists(dae):
         return None
@@ -81,8 +124,8 @@ def cpu_baseline_reference(dae: str, name: str, threads: int, budget_s: float = 
     with tempfile.TemporaryDirectory() as td:
         while t_tot < budget_s * 0.6 and runs < 3:
             r = subprocess.run([REF_DRIVER, "-s", str(spp_run), "-t", str(threads), "-m", str(M), "-r", str(W),
-                                str(H), "-f", os.path.join(td, "ref.png"), dae], capture_output=True,
-                               text=True, timeout=600, cwd=td)
+                                str(H), "-f", os.path.join(td, "ref.png"), os.path.abspath(dae)],
+                               capture_output=True, text=True, timeout=600, cwd=td)
             m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", r.stdout)
             if r.returncode != 0 or not m:
                 return None
@@ -98,9 +141,9 @@ def cpu_baseline_reference(dae: str, name: str, threads: int, budget_s: float = 
                       f"{t_tot:.1f} s of rendering"}
 
 
-def parity_check(scene, seed: int, rr: bool = False) -> dict:
+def parity_check(scene, W: int, H: int, M: int, seed: int, rr: bool = False) -> dict:
     """Per-pixel RMSE of the GPU sample buffer vs the oracle's COUNTER32 CPU path, same seed,
-    same workload at 2 spp (the CPU side of the metric)."""
+    same frame at 2 spp (the CPU side of the metric)."""
     import numpy as np
     import bdpt_amd as B
     from _util import MODE_C32, oracle_render
@@ -111,25 +154,46 @@ def parity_check(scene, seed: int, rr: bool = False) -> dict:
     pt.close()
     ref = oracle_render(scene, W, H, S, M, MODE_C32, seed=seed,
                         threads=min(16, os.cpu_count() or 1), rr=rr)[0]
-    return {"rmse": float(np.sqrt(np.mean((g - ref) ** 2))), "spp": S, "tolerance": 1e-4,
-            "cpu": "oracle COUNTER32 (fp32 device semantics)"}
+    return {"rmse": float(np.sqrt(np.mean((g - ref) ** 2))), "spp": S, "frame": f"{W}x{H}",
+            "tolerance": 1e-4, "cpu": "oracle COUNTER32 (fp32 device semantics)"}
+
+
+def load_traffic(workload: str, kernel_ms: float):
+    """HBM-side bytes of one launch of this workload from the committed PMC passes
+    (profiles/traffic_<workload>.json: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc runs of
+    tools/prof_render.py, reduced by tools/pmc_traffic.py). Counters cannot be collected inside the
+    timed process (rocprofv3 wraps the whole program), so the file records which run it came from."""
+    path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        rec = json.load(f)
+    b = rec.get("hbm_bytes_per_launch")
+    if not b:
+        return None, None
+    gbps = b / (kernel_ms * 1e-3) / 1e9
+    return b, {"source": os.path.relpath(path, REPO), "read_bytes": rec.get("hbm_read_bytes"),
+               "write_bytes": rec.get("hbm_write_bytes"), "gbps_at_this_kernel_ms": round(gbps, 2),
+               "frac": round(gbps / HBM_PEAK_GBPS, 5), "pmc_kernel_ms": rec.get("kernel_ms")}
 
 
 def main() -> int:
-    global W, H, SPP, M
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="ns",
+                    help="ns = the north-star target (default); c2..c5 = BASELINE.json configs[1..4]")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: the workload's fixed render split across ranks (default); "
+                         "weak: every rank renders the full spp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--scene", default=SCENE,
-                    help="golden scene name (tests/golden/scenes) or a .dae path, e.g. the north-star "
-                         "stand-in scenes/CBlucy_standin.dae")
-    ap.add_argument("--width", type=int, default=W)
-    ap.add_argument("--height", type=int, default=H)
-    ap.add_argument("--spp", type=int, default=SPP)
-    ap.add_argument("--max-depth", type=int, default=M)
+    ap.add_argument("--scene", default=None, help="override: a .dae path")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--max-depth", type=int, default=None)
     ap.add_argument("--pipeline", type=int, default=0, help="0 auto, 1 megakernel, 2 wavefront")
     ap.add_argument("--envmap", default=None,
                     help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
@@ -140,12 +204,21 @@ def main() -> int:
                          "unidirectional PathTracer, DESIGN.md §10; adaptive sampling off: every "
                          "pixel takes all spp; ranks split the frame into row bands)")
     args = ap.parse_args()
-    W, H, SPP, M = args.width, args.height, args.spp, args.max_depth
+    wl = WORKLOADS[args.workload]
+    scene_path = args.scene or os.path.join(REPO, wl[0])
+    W = args.width or wl[1]
+    H = args.height or wl[2]
+    SPP = args.spp or wl[3]
+    M = args.max_depth if args.max_depth is not None else wl[4]
+    envmap = args.envmap if args.envmap is not None else wl[5]
+    rr = args.rr or wl[6]
+    named = (args.scene is None and args.width is None and args.height is None and args.spp is None
+             and args.max_depth is None and args.envmap is None and not args.rr)
+    ensure_standin(scene_path)
 
     import numpy as np
     import torch
     import bdpt_amd as B
-    from _util import golden_scene
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -159,48 +232,50 @@ def main() -> int:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    scene = (B.load_dae(args.scene, W, H) if args.scene.endswith(".dae")
-             else golden_scene(args.scene, W, H))
+    t_load = time.perf_counter()
+    scene = B.load_dae(scene_path, W, H)      # bdpt_dae_load: the CLI's scene path
+    t_load = time.perf_counter() - t_load
     env_desc = None
-    if args.envmap:
-        if args.envmap.startswith("synth:"):
+    if envmap:
+        if envmap.startswith("synth:"):
             sys.path.insert(0, os.path.join(REPO, "tools"))
             from envmap import synth_envmap
-            ew, eh = (int(v) for v in args.envmap[6:].split("x"))
+            ew, eh = (int(v) for v in envmap[6:].split("x"))
             scene.set_envmap(synth_envmap(ew, eh))
             env_desc = f"synthetic sky {ew}x{eh} (tools/envmap.py)"
         else:
-            scene.set_envmap(B.load_exr(args.envmap))
-            env_desc = os.path.basename(args.envmap)
+            scene.set_envmap(B.load_exr(envmap))
+            env_desc = os.path.basename(envmap)
     seed = 5489
     stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
     torch.cuda.set_stream(stream)
-    # weight 1/(world*SPP): the N-GPU image is an N*128-spp render
     use_pt = args.integrator == "pt"
+    scaling = "strong" if use_pt else args.scaling
     band = [(0, H * rank // world, W, H * (rank + 1) // world - H * rank // world)]
+    t_create = time.perf_counter()
     if use_pt:   # whole pixels: each rank renders its row band with all SPP samples
         pt = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index, max_tolerance=0.0)
     else:
-        pt = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                       pipeline=args.pipeline, russian_roulette=args.rr)
+        # sample weight 1/ns_aa: strong = the workload's spp, weak = the N-GPU image of N*spp
+        pt = B.BidirectionalPathTracer(scene, W, H, SPP if scaling == "strong" else SPP * world, M, seed=seed,
+                                       device=dev.index, pipeline=args.pipeline, russian_roulette=rr)
     pt.set_stream(stream.cuda_stream)
+    t_create = time.perf_counter() - t_create
     frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
 
     def render(k: int):
         if use_pt:
             pt.raytrace_tiles(band, 0, SPP)
         else:
-            base, n = rank_sample_range(k, rank, world, SPP)   # fresh global sample range every step
-            pt.raytrace_tiles([], base, n)
+            base, n = rank_sample_range(k, rank, world, SPP, scaling)
+            if n > 0:
+                pt.raytrace_tiles([], base, n)
 
-    def step(k: int):
+    for k in range(args.warmup):
         render(k)
         pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
         if dist is not None:
             dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
-
-    for k in range(args.warmup):
-        step(k)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -222,47 +297,47 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_samples = int(pt.read_sample_counts().astype(np.int64)[band[0][1]:band[0][1] + band[0][3]].sum()) \
-        if use_pt else W * H * SPP
+        if use_pt else W * H * rank_sample_range(0, rank, world, SPP, scaling)[1]
+    rank_elapsed, rank_kern = [elapsed], [kern_ms]
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.tensor([elapsed, kern_ms, float(rank_samples)], dtype=torch.float64, device=dev)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rank_elapsed = [float(x[0]) for x in allt]
+        rank_kern = [float(x[1]) for x in allt]
+        elapsed = max(rank_elapsed)
+        samples_per_step = sum(float(x[2]) for x in allt)
+    else:
+        samples_per_step = float(rank_samples)
     pt.close()
 
-    # algorithmic bytes of one launch: in-kernel counters on a separate, untimed launch of the
-    # same workload (counting perturbs timing), SURVEY.md §8d.
+    # algorithmic bytes of this rank's launch: in-kernel counters on a separate, untimed launch of
+    # the same work (counting perturbs timing), SURVEY.md §8d.
     if use_pt:
         ps = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index, max_tolerance=0.0,
                           collect_stats=True)
         ps.raytrace_tiles(band, 0, SPP)
     else:
-        ps = B.BidirectionalPathTracer(scene, W, H, SPP * world, M, seed=seed, device=dev.index,
-                                       collect_stats=True, pipeline=args.pipeline, russian_roulette=args.rr)
-        ps.raytrace_tiles([], rank * SPP, SPP)
+        ps = B.BidirectionalPathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index,
+                                       collect_stats=True, pipeline=args.pipeline, russian_roulette=rr)
+        b0, n0 = rank_sample_range(0, rank, world, SPP, scaling)
+        ps.raytrace_tiles([], b0, max(1, n0))
     st = ps.stats()
     ps.close()
     bytes_launch = algorithmic_bytes(st)
+    gmem_launch = global_memory_bytes(st)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-
-    if dist is not None and use_pt:
-        t = torch.tensor([rank_samples], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        samples_total = float(t.item()) * args.steps
-    else:
-        samples_total = (rank_samples if use_pt else W * H * SPP * world) * args.steps
-    value = samples_total / elapsed / 1e6
-    traffic = None
-    default_workload = ((args.scene, W, H, SPP, M) == (SCENE, 480, 360, 128, 5) and not args.envmap
-                        and not args.rr and not use_pt)
-    tpath = os.path.join(REPO, "profiles", "traffic_r01.json")   # PMC pass of this workload
-    if default_workload and os.path.exists(tpath):
-        with open(tpath) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    value = samples_per_step * args.steps / elapsed / 1e6
+    traffic, traffic_info = (None, None)
+    if world == 1 and named and not use_pt and args.pipeline == 0:
+        traffic, traffic_info = load_traffic(args.workload, kern_ms)
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return 0
+    wname = wl[7] if named else (f"{os.path.basename(scene_path)} {W}x{H} -s {SPP} -m {M}"
+                                 f"{' + env ' + env_desc if env_desc else ''}{' RR on' if rr else ''}")
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -272,44 +347,58 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": f"synthetic: fixed-seed renders (Philox counter RNG) of the reference's scene "
-                f"{os.path.basename(args.scene)} as the reference loads it",
-        "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} -s {SPP} -m {M}"
-                               f"{' + env ' + env_desc if env_desc else ''}{' RR on' if args.rr else ''}"
-                               f"{' unidirectional PathTracer' if use_pt else ''}"
-                               f"{' (BASELINE configs[1])' if default_workload else ''} "
-                               + ("for the whole frame, row bands per GPU + RCCL sum-reduce" if use_pt else
-                                  "per GPU, sample-range shards + RCCL sum-reduce"),
+        "data": f"synthetic: fixed-seed renders (Philox counter RNG) of {os.path.basename(scene_path)} "
+                f"loaded by the product's .dae loader (bdpt_dae_load)"
+                + ("; CBlucy.dae is absent from the reference, its stand-in (tools/gen_standin.py, "
+                   "114,304 triangles) is rendered" if os.path.basename(scene_path) == os.path.basename(STANDIN) else ""),
+        "config": {"workload": wname
+                   + (" unidirectional PathTracer" if use_pt else "")
+                   + (", whole frame per step split across GPUs" if scaling == "strong" else ", full spp per GPU")
+                   + (" (row bands)" if use_pt else " (sample ranges)") + " + RCCL sum-reduce",
+                   "workload_key": args.workload if named else "custom",
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
-                   "scene": args.scene, "width": W, "height": H, "spp_per_gpu": SPP,
-                   "max_depth": M, "envmap": env_desc, "russian_roulette": args.rr,
-                   "parallelism": f"samples x{world}"},
+                   "scene": os.path.relpath(scene_path, REPO), "width": W, "height": H, "spp": SPP,
+                   "max_depth": M, "envmap": env_desc, "russian_roulette": rr,
+                   "parallelism": f"{'row bands' if use_pt else 'sample ranges'} x{world}",
+                   "host_setup_s": {"dae_load": round(t_load, 3), "bdpt_create": round(t_create, 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                      "traffic": traffic, "kernel": "k_pt" if use_pt else "k_bdpt_sample",
                      "kernel_ms": round(kern_ms, 3),
                      "algorithmic_bytes_per_launch": bytes_launch,
-                     "counts_per_launch": {"node_aabbs": st.node_visits, "tri_tests": st.tri_tests,
+                     "note": "achieved = SURVEY §8d algorithmic scene bytes (32 B/child AABB, 36 B/triangle "
+                             "test, 16 B/sphere test, 40 B/closest hit) / launch time (HIP events on the ctx "
+                             "stream); gmem_* leaves out the scene reads served from the CU's LDS copy; "
+                             "traffic = measured HBM-side bytes (PMC)",
+                     "gmem_bytes_per_launch": gmem_launch,
+                     "gmem_achieved": round(gmem_launch / (kern_ms * 1e-3) / 1e9, 2),
+                     "gmem_frac": round(gmem_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+                     "lds_mode": st.lds_mode,
+                     "counts_per_launch": {"samples": st.samples, "node_aabbs": st.node_visits,
+                                           "node_aabbs_from_lds": st.lds_node_visits,
+                                           "tri_tests": st.tri_tests,
                                            "sph_tests": st.sph_tests, "hits": st.hits,
                                            "closest_rays": st.closest_rays,
                                            "shadow_rays": st.shadow_rays}},
     }
+    if traffic_info:
+        out["roofline"]["traffic_pmc"] = traffic_info
+    if world > 1:
+        out["per_rank"] = {"elapsed_s": [round(x, 4) for x in rank_elapsed],
+                           "kernel_ms": [round(x, 3) for x in rank_kern]}
     if use_pt:
         out["config"]["integrator"] = "PathTracer (pathtracer.cpp:47-340)"
-        out["config"]["parallelism"] = f"row bands x{world}"
-        out["scaling"] = "strong"
     if world == 1 and not args.no_parity and not use_pt:
-        out["parity"] = parity_check(scene, seed, rr=args.rr)
+        out["parity"] = parity_check(scene, W, H, M, seed, rr=rr)
     if world == 1 and not args.no_cpu_baseline and not use_pt:
         thr = min(16, os.cpu_count() or 1)
-        dae = args.scene if args.scene.endswith(".dae") else os.path.join(REPO, "scenes", args.scene + ".dae")
-        port = cpu_baseline(scene, args.scene, threads=thr, rr=args.rr)
+        port = cpu_baseline(scene, os.path.basename(scene_path), W, H, SPP, M, threads=thr, rr=rr)
         # the reference cannot run the environment light / roulette under BDPT: port only
-        ref = (None if (args.envmap or args.rr)
-               else cpu_baseline_reference(dae, os.path.basename(args.scene), threads=thr))
+        ref = (None if (env_desc or rr)
+               else cpu_baseline_reference(scene_path, os.path.basename(scene_path), W, H, M, threads=thr))
         out["cpu_baseline"] = ref if ref is not None else port
         if ref is not None:   # the oracle port's fp64 path, same host, for comparison
             out["cpu_baseline"]["port"] = {"value": port["value"], "cores": port["cores"], "sample": port["sample"]}

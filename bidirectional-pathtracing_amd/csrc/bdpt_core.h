@@ -266,6 +266,7 @@ struct SceneView {
 // Counters for the roofline (algorithmic bytes)
 struct Counters {
   uint32_t nodes, tris, sphs, closest, shadow, hits;
+  uint32_t lnodes = 0;   // of `nodes`: child AABBs read from the block's LDS copy (LM 1, LM 2 treelet)
 #ifdef BDPT_PHASE_PROF
   unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
 #endif
@@ -537,8 +538,10 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
   if (LM == 1) {   // all nodes in LDS: plain ds_reads the compiler schedules
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
+    c.lnodes += W;
   } else if (LM == 2 && ref < S.ntop) {
     ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
+    c.lnodes += W;
   } else {
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 
 #include "bdpt/bdpt.h"
@@ -44,10 +45,26 @@ struct Ctx {
   float* d_light = nullptr;
   float* d_sample = nullptr;
   unsigned long long* d_stats = nullptr;   // [0..6] counters, [8..10] phase cycles, [15] tickets
-  int4* d_blocks = nullptr;
-  size_t blocks_cap = 0;
-  int4* h_blocks = nullptr;   // pinned staging
-  size_t h_blocks_cap = 0;
+  // Tile-block lists of bdpt_render: a ring of pinned staging + device buffers, each slot reused
+  // only after the event recorded behind the launch that read it, so back-to-back tile renders
+  // (raytrace_tile / raytrace_pixel callers) never wait for the GPU.
+  struct BlockSlot {
+    int4* h = nullptr;
+    int4* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+  };
+  static constexpr int kBlockSlots = 4;
+  BlockSlot blk[kBlockSlots];
+  int blk_next = 0;
+  // Every entry point locks the ctx: the reference drives raytrace_pixel / raytrace_tile from N
+  // worker threads (raytraced_renderer.cpp:325-327,610-615); calls on one ctx are serialised here.
+  std::recursive_mutex mu;
+  // Diagnostics read once at bdpt_create (BDPT_LDS_MODE, BDPT_NTOP_MAX, BDPT_BLOCK_MAJOR,
+  // BDPT_XCD_GROUPS, BDPT_PIPELINE): -1 = not set.
+  int env_lds_mode = -1, env_ntop_max = -1, block_major = 1, xcd = 0;
+  int last_lm = -1;            // LDS mode of the last BDPT / PathTracer launch
   int maxv = 5;
   int ncu = 256;
   size_t npix = 0;

@@ -527,9 +527,9 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   }
 #endif
   if (STATS) {
-    unsigned v[7] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits};
+    unsigned v[8] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes};
 #pragma unroll
-    for (int k = 0; k < 7; k++) {
+    for (int k = 0; k < 8; k++) {
       unsigned s = wave_sum(v[k]);
       if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
     }
@@ -603,9 +603,9 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_pt(PtKParams kp)
     }
   }
   if (STATS) {
-    unsigned v[7] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits};
+    unsigned v[8] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes};
 #pragma unroll
-    for (int k = 0; k < 7; k++) {
+    for (int k = 0; k < 8; k++) {
       unsigned s = wave_sum(v[k]);
       if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
     }
@@ -666,10 +666,9 @@ int launch_lm(Ctx* c, KParams& kp) {
   const size_t q = kWavesPerBlock * sizeof(WaveQ);
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const bool has_nodes = !c->hs.bvh2.nodes.empty();
-  const char* env = getenv("BDPT_LDS_MODE");   // diagnostics: force 0 / 1 / 2 / 3
   // LM 3's LDS: geometry, leaf list (padded to 16 B), shading records
   const size_t flat = 2 * c->hs.geom.size() * sizeof(float) + (c->hs.leaf_refs.size() + 3) / 4 * 16;
-  int lm = env ? atoi(env)
+  int lm = c->env_lds_mode >= 0 ? c->env_lds_mode   // diagnostics: BDPT_LDS_MODE forces 0 / 1 / 2 / 3
                : (c->hs.nprim <= kFlatMaxPrims && flat <= kLdsSceneMax) ? 3
                : (full <= kLdsSceneMax ? 1 : has_nodes ? 2 : 0);
   if (lm == 3 && flat > kLdsSceneMax) lm = 1;
@@ -678,7 +677,8 @@ int launch_lm(Ctx* c, KParams& kp) {
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
-  if (lm == 2 && getenv("BDPT_NTOP_MAX")) kp.S.ntop = std::min(kp.S.ntop, atoi(getenv("BDPT_NTOP_MAX")));   // diagnostics
+  if (lm == 2 && c->env_ntop_max >= 0) kp.S.ntop = std::min(kp.S.ntop, c->env_ntop_max);   // diagnostics
+  c->last_lm = lm;
   if (lm == 3) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 3, EXT>, q + flat, kp);
   if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, q + full, kp);
   if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
@@ -706,12 +706,13 @@ template <bool STATS>
 int launch_pt(Ctx* c, PtKParams& kp) {
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const size_t lds_max = kLdsPerCu / kBlocksPerCu - 256;
-  const char* env = getenv("BDPT_LDS_MODE");
   // LM 3's LDS: geometry, leaf list (padded to 16 B), shading records
   const size_t flat = 2 * c->hs.geom.size() * sizeof(float) + (c->hs.leaf_refs.size() + 3) / 4 * 16;
-  int lm = env ? atoi(env) : (c->hs.nprim <= kFlatMaxPrims && flat <= lds_max) ? 3 : (full <= lds_max ? 1 : 2);
+  int lm = c->env_lds_mode >= 0 ? c->env_lds_mode
+               : (c->hs.nprim <= kFlatMaxPrims && flat <= lds_max) ? 3 : (full <= lds_max ? 1 : 2);
   if (lm == 3 && flat > lds_max) lm = 1;
   if (lm == 1 && full > lds_max) lm = 2;
+  c->last_lm = lm;
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
@@ -725,11 +726,15 @@ int launch_pt(Ctx* c, PtKParams& kp) {
 void free_ctx(Ctx* c) {
   if (!c) return;
   void* bufs[] = {c->d_nodes2, c->d_nodes4, c->d_geom, c->d_shade, c->d_mats, c->d_lights, c->d_prim_ref, c->d_env, c->d_count, c->d_work8, c->d_leaves,
-                  c->d_eye, c->d_light, c->d_sample, c->d_stats, c->d_blocks};
+                  c->d_eye, c->d_light, c->d_sample, c->d_stats};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   wf_free(c);
-  if (c->h_blocks) (void)hipHostFree(c->h_blocks);
+  for (Ctx::BlockSlot& b : c->blk) {
+    if (b.d) (void)hipFree(b.d);
+    if (b.h) (void)hipHostFree(b.h);
+    if (b.done) (void)hipEventDestroy(b.done);
+  }
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -768,6 +773,13 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   // megakernel, 2 = wavefront. BDPT_PIPELINE overrides (diagnostics / A-B runs).
   int pipe = p.pipeline;
   if (const char* pe = getenv("BDPT_PIPELINE")) pipe = atoi(pe);
+  // diagnostics / A-B switches, read once per ctx (tests set them before bdpt_create)
+  auto env_int = [](const char* name, int dflt) { const char* v = getenv(name); return v ? atoi(v) : dflt; };
+  c->env_lds_mode = env_int("BDPT_LDS_MODE", -1);
+  c->env_ntop_max = env_int("BDPT_NTOP_MAX", -1);
+  c->block_major = env_int("BDPT_BLOCK_MAJOR", 1);
+  c->xcd = env_int("BDPT_XCD_GROUPS", 0);
+  if (c->env_lds_mode > 3) { g_err = "BDPT_LDS_MODE must be 0..3"; delete c; return BDPT_E_INVALID; }
   c->pipeline = pipe == 2 ? PIPE_WAVEFRONT : PIPE_MEGAKERNEL;
   c->pt = p.integrator == BDPT_INTEGRATOR_PT;
   if (p.integrator != BDPT_INTEGRATOR_BDPT && !c->pt) { g_err = "unknown integrator"; delete c; return BDPT_E_INVALID; }
@@ -813,7 +825,9 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
     g_err = "out of device memory";
     return fail(BDPT_E_NOMEM);
   }
-  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+  bool ev_ok = true;
+  for (Ctx::BlockSlot& b : c->blk) ev_ok = ev_ok && hipEventCreateWithFlags(&b.done, hipEventDisableTiming) == hipSuccess;
+  if (!ev_ok || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     g_err = "stream/event creation failed";
     return fail(BDPT_E_DEVICE);
@@ -831,14 +845,18 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
 void bdpt_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  {
+    std::lock_guard<std::recursive_mutex> lk(c->mu);   // waits for a call in flight on another thread
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+  }
   free_ctx(c);
 }
 
 int bdpt_set_stream(void* ctx, void* stream) {
   Ctx* c = (Ctx*)ctx;
   if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   c->stream = stream ? (hipStream_t)stream : c->own;
   return BDPT_OK;
 }
@@ -846,6 +864,7 @@ int bdpt_set_stream(void* ctx, void* stream) {
 int bdpt_clear(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   size_t fb = c->npix * 3 * sizeof(float);
   HIPCHK(hipMemsetAsync(c->d_eye, 0, fb, c->stream));
@@ -859,7 +878,9 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   Ctx* c = (Ctx*)ctx;
   if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
   if (spp_begin < 0 || spp_count < 0 || ntiles < 0) { g_err = "negative argument"; return BDPT_E_INVALID; }
+  if ((int64_t)spp_begin + spp_count > INT32_MAX) { g_err = "spp_begin + spp_count overflows int32"; return BDPT_E_INVALID; }
   if (spp_count == 0) return BDPT_OK;
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   const int W = c->prm.width, H = c->prm.height;
   KParams kp;
@@ -875,6 +896,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);
+  Ctx::BlockSlot* slot = nullptr;
   if (tiles && ntiles > 0) {
     // Tiles (raytrace_tile clips them to the frame, raytraced_renderer.cpp:600-604) -> 8x8 blocks.
     std::vector<int4> blk;
@@ -885,21 +907,33 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
         for (int bx = x0; bx < x1; bx += 8) blk.push_back(make_int4(bx, by, std::min(8, x1 - bx), std::min(8, y1 - by)));
     }
     if (blk.empty()) return BDPT_OK;
-    if (blk.size() > c->blocks_cap) {
-      HIPCHK(hipStreamSynchronize(c->stream));
-      if (c->d_blocks) (void)hipFree(c->d_blocks);
-      if (c->h_blocks) (void)hipHostFree(c->h_blocks);
-      c->blocks_cap = blk.size();
-      HIPCHK(hipMalloc((void**)&c->d_blocks, c->blocks_cap * sizeof(int4)));
-      HIPCHK(hipHostMalloc((void**)&c->h_blocks, c->blocks_cap * sizeof(int4)));
-    } else {
-      HIPCHK(hipStreamSynchronize(c->stream));   // staging buffer reuse
+    // next slot of the staging ring: wait only for the launch that last read it
+    slot = &c->blk[c->blk_next];
+    c->blk_next = (c->blk_next + 1) % Ctx::kBlockSlots;
+    if (slot->pending) HIPCHK(hipEventSynchronize(slot->done));
+    slot->pending = false;
+    if (blk.size() > slot->cap) {
+      if (slot->d) { (void)hipFree(slot->d); slot->d = nullptr; }
+      if (slot->h) { (void)hipHostFree(slot->h); slot->h = nullptr; }
+      slot->cap = 0;
+      HIPCHK(hipMalloc((void**)&slot->d, blk.size() * sizeof(int4)));
+      HIPCHK(hipHostMalloc((void**)&slot->h, blk.size() * sizeof(int4)));
+      slot->cap = blk.size();
     }
-    memcpy(c->h_blocks, blk.data(), blk.size() * sizeof(int4));
-    HIPCHK(hipMemcpyAsync(c->d_blocks, c->h_blocks, blk.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
-    kp.blocks = c->d_blocks;
+    memcpy(slot->h, blk.data(), blk.size() * sizeof(int4));
+    HIPCHK(hipMemcpyAsync(slot->d, slot->h, blk.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    kp.blocks = slot->d;
     kp.nblocks = (int)blk.size();
   }
+  // the slot is free again once everything enqueued below has run (on every return path)
+  struct SlotRelease {
+    Ctx::BlockSlot* s;
+    hipStream_t st;
+    ~SlotRelease() {
+      if (s && hipEventRecord(s->done, st) == hipSuccess) s->pending = true;
+      else if (s) (void)hipStreamSynchronize(st);
+    }
+  } slot_release{slot, c->stream};
   if (c->pt) {   // the PathTracer renders whole pixels (adaptive sampling decides per pixel)
     if (spp_begin != 0 || spp_count != c->prm.spp) {
       g_err = "the PathTracer renders whole pixels: spp_begin must be 0 and spp_count the ctx's spp";
@@ -955,12 +989,12 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.nchunks = (unsigned)nchunks;
   // consecutive tickets take one pixel block's sample chunks in turn (measured: C2 +1.2%, CBgems
   // +2%, Lucy stand-in 1080p +-0 over chunk-major order); BDPT_BLOCK_MAJOR=0 restores chunk-major
-  kp.block_major = getenv("BDPT_BLOCK_MAJOR") ? atoi(getenv("BDPT_BLOCK_MAJOR")) : 1;
+  kp.block_major = c->block_major;
   kp.work = (unsigned*)(c->d_stats + 15);
   HIPCHK(hipMemsetAsync(kp.work, 0, sizeof(unsigned), c->stream));
   kp.work8 = c->d_work8;
   kp.region = (kp.nitems + 7u) / 8u;
-  kp.xcd = getenv("BDPT_XCD_GROUPS") ? atoi(getenv("BDPT_XCD_GROUPS")) : 0;
+  kp.xcd = c->xcd;
   if (kp.xcd) HIPCHK(hipMemsetAsync(kp.work8, 0, 8 * 32 * sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp) : launch_maxv<16>(c, kp);
@@ -973,6 +1007,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
 int bdpt_sync(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) { g_err = "null ctx"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   return BDPT_OK;
@@ -981,6 +1016,7 @@ int bdpt_sync(void* ctx) {
 int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !dptr) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (which == BDPT_FRAME_EYE) { *dptr = c->d_eye; return BDPT_OK; }
   if (which == BDPT_FRAME_LIGHT) { *dptr = c->d_light; return BDPT_OK; }
@@ -996,6 +1032,7 @@ int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr) {
 int bdpt_copy_frame(void* ctx, int32_t which, void* dst_device) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !dst_device) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   void* p = nullptr;
   int rc = bdpt_frame_device_ptr(ctx, which, &p);
   if (rc) return rc;
@@ -1006,6 +1043,7 @@ int bdpt_copy_frame(void* ctx, int32_t which, void* dst_device) {
 int bdpt_read_frame(void* ctx, int32_t which, float* rgb) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !rgb) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   void* p = nullptr;
   int rc = bdpt_frame_device_ptr(ctx, which, &p);
   if (rc) return rc;
@@ -1017,6 +1055,7 @@ int bdpt_read_frame(void* ctx, int32_t which, float* rgb) {
 int bdpt_read_sample_counts(void* ctx, int32_t* counts) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !counts) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->pt) {
@@ -1030,6 +1069,7 @@ int bdpt_read_sample_counts(void* ctx, int32_t* counts) {
 int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !out) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   unsigned long long s[8];
@@ -1048,12 +1088,15 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   out->last_kernel_ms = ms;
   out->bvh_nodes = (uint64_t)c->hs.ref_nodes;
   out->bvh_depth = (uint64_t)c->hs.depth;
+  out->lds_node_visits = s[7];
+  out->lds_mode = c->last_lm;
   return BDPT_OK;
 }
 
 int bdpt_debug_counters(void* ctx, uint64_t* out16) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !out16) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out16, c->d_stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1064,9 +1107,14 @@ int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, fl
   Ctx* c = (Ctx*)ctx;
   if (!c || (!rays && n) || n < 0) { g_err = "bad argument"; return BDPT_E_INVALID; }
   if (n == 0) return BDPT_OK;
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   float *d_r = nullptr, *d_t = nullptr;
   int* d_p = nullptr;
+  struct Frees {   // every exit path (HIPCHK returns early) releases the temporaries
+    void** p[3];
+    ~Frees() { for (void** q : p) if (*q) (void)hipFree(*q); }
+  } frees{{(void**)&d_r, (void**)&d_t, (void**)&d_p}};
   HIPCHK(hipMalloc((void**)&d_r, (size_t)n * 8 * sizeof(float)));
   HIPCHK(hipMalloc((void**)&d_t, (size_t)n * sizeof(float)));
   HIPCHK(hipMalloc((void**)&d_p, (size_t)n * sizeof(int)));
@@ -1077,9 +1125,6 @@ int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, fl
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(out_t, d_t, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(out_prim, d_p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
-  (void)hipFree(d_r);
-  (void)hipFree(d_t);
-  (void)hipFree(d_p);
   return BDPT_OK;
 }
 

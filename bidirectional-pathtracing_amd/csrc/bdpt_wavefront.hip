@@ -153,9 +153,9 @@ struct QView {
 };
 
 __device__ __forceinline__ void flush_stats(unsigned long long* st, unsigned samples, const Counters& c) {
-  unsigned v[7] = {samples, c.closest, c.shadow, c.nodes, c.tris, c.sphs, c.hits};
+  unsigned v[8] = {samples, c.closest, c.shadow, c.nodes, c.tris, c.sphs, c.hits, c.lnodes};
 #pragma unroll
-  for (int k = 0; k < 7; k++) {
+  for (int k = 0; k < 8; k++) {
     unsigned s = wave_sum_u(v[k]);
     if (lane_id() == 0 && s) atomicAdd(st + k, (unsigned long long)s);
   }

@@ -11,7 +11,14 @@
  *   BidirectionalPathTracer::{sampleBuffer, eyeBuffer, lightBuffer}
  *     (bidirection.h:81, pathtracer.h:90)         -> bdpt_read_frame (BDPT_FRAME_*)
  *   RaytracedRenderer::set_scene / build_accel    -> bdpt_create (scene desc; the BVH is built
- *     (raytraced_renderer.cpp:105-127,350-374)       inside, reference midpoint split, bvh.cpp:51-129)
+ *     (raytraced_renderer.cpp:105-127,350-374)       inside: the reference's midpoint-split tree,
+ *                                                    bvh.cpp:51-129, for its DFS leaf order (the
+ *                                                    equal-t tie key), and a binned-SAH device tree
+ *                                                    over the same primitives)
+ *
+ * Threading: one ctx per GPU. Every entry point taking a ctx locks it, so the reference's model of
+ * N worker threads calling raytrace_pixel / raytrace_tile on one PathTracer
+ * (raytraced_renderer.cpp:325-327,610-615) is safe; the calls are serialised per ctx.
  *
  * Plain C types only: no torch, no HIP types in any signature (a stream is passed as void*).
  * Every call returns 0 (BDPT_OK) or a negative BDPT_E_* code; bdpt_last_error() gives the text.
@@ -40,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 3
+#define BDPT_ABI_VERSION 4
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -173,6 +180,11 @@ typedef struct bdpt_stats {
   double last_kernel_ms;      /* duration of the last bdpt_render's kernels (hipEvents)  */
   uint64_t bvh_nodes;
   uint64_t bvh_depth;
+  /* ABI v4: where the scene reads of the last launches were served from */
+  uint64_t lds_node_visits;   /* of node_visits: AABBs read from the CU's LDS copy          */
+  int32_t lds_mode;           /* 0 scene in HBM, 1 whole scene in LDS, 2 BFS treelet in LDS +
+                                 HBM below it, 3 flat primitive list in LDS; -1 none yet     */
+  int32_t reserved0;
 } bdpt_stats;
 
 int bdpt_abi_version(void);

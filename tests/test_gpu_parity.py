@@ -268,3 +268,141 @@ def test_lds_modes_agree_c2(lds, monkeypatch):
     g = _gpu_render(sc, W, H, S, M)
     samp = oracle_render(sc, W, H, S, M, MODE_C32)[0]
     assert _rmse(g["sample"], samp) < RMSE_TOL
+
+
+# --- the north-star kernel path: the CBlucy stand-in (114,304 triangles) ---------------------------
+# The device BVH4 (73k nodes) does not fit in LDS: the default LDS mode 2 stages its first 1024
+# BFS nodes (the treelet every ray starts in) and reads the rest from HBM; these cases cover that
+# hand-off, deep stacks and the C3 / north-star / C5 frame sizes (BASELINE configs).
+def _standin(W, H):
+    import os
+    import sys
+    from _util import REPO
+    sys.path.insert(0, REPO)
+    from bench import STANDIN, ensure_standin
+    path = os.path.join(REPO, STANDIN)
+    ensure_standin(path)
+    return B.load_dae(path, W, H)
+
+
+def _check_frames(g, ref, label):
+    samp, eye, light = ref[0], ref[1], ref[2]
+    assert np.isfinite(g["sample"]).all()
+    r, re_, rl = _rmse(g["sample"], samp), _rmse(g["eye"], eye), _rmse(g["light"], light)
+    print(f"{label}: rmse sample {r:.3e} eye {re_:.3e} light {rl:.3e} mean gpu {g['sample'].mean():.6f} "
+          f"oracle {samp.mean():.6f}")
+    assert r < RMSE_TOL and re_ < RMSE_TOL and rl < RMSE_TOL
+
+
+def test_standin_c3_frame_default_mode():
+    """C3's frame (800x600, m=5) at 2 spp through the default path: LDS mode 2 (treelet in LDS,
+    BVH4 below it in HBM); the stats show both kinds of node fetch."""
+    W, H, S, M = 800, 600, 2, 5
+    sc = _standin(W, H)
+    g = _gpu_render(sc, W, H, S, M, stats=True)
+    st = g["stats"]
+    assert st.lds_mode == 2
+    assert 0 < st.lds_node_visits < st.node_visits
+    _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32), "stand-in 800x600 s2 m5")
+
+
+def test_standin_northstar_frame_and_tiles():
+    """The north-star frame (1920x1080, m=5, FOV quirk at 1080p) at 1 spp, full frame vs the
+    oracle; then a subset of 32x32 tiles (raytrace_tile): their eye image equals the full render's
+    on those pixels (a pixel's eye value depends on its own samples only)."""
+    W, H, S, M = 1920, 1080, 1, 5
+    sc = _standin(W, H)
+    ref = oracle_render(sc, W, H, S, M, MODE_C32)
+    g = _gpu_render(sc, W, H, S, M)
+    _check_frames(g, ref, "stand-in 1920x1080 s1 m5")
+    tiles = [(x, y, 32, 32) for y in range(0, H, 32) for x in range(0, W, 32) if (x // 32 + 3 * (y // 32)) % 7 == 0]
+    gt = _gpu_render(sc, W, H, S, M, tiles=tiles)
+    mask = np.zeros((H, W), bool)
+    for x, y, w, h in tiles:
+        mask[y:y + h, x:x + w] = True
+    assert _rmse(gt["eye"][mask], ref[1][mask]) < RMSE_TOL
+    assert np.all(gt["eye"][~mask] == 0)
+
+
+@pytest.mark.parametrize("lds,ntop", [("0", None), ("2", None), ("2", "64"), ("2", "1")])
+def test_standin_lds_modes(lds, ntop, monkeypatch):
+    """Scene wholly in HBM (LM 0) and treelets of 1024 / 64 / 1 nodes (BDPT_NTOP_MAX) in front of
+    the HBM part: the hand-off depth changes, the image does not."""
+    monkeypatch.setenv("BDPT_LDS_MODE", lds)
+    if ntop:
+        monkeypatch.setenv("BDPT_NTOP_MAX", ntop)
+    W, H, S, M = 320, 240, 2, 5
+    sc = _standin(W, H)
+    g = _gpu_render(sc, W, H, S, M, stats=True)
+    assert g["stats"].lds_mode == int(lds)
+    _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32), f"stand-in LM {lds} ntop {ntop}")
+
+
+@pytest.mark.parametrize("lds", ["0", "2"])
+def test_standin_c5_shaped(lds, monkeypatch):
+    """C5's shape at a small frame: the stand-in + an environment light + Russian roulette at m=8
+    (EXT kernel) with the mesh BVH from HBM / the treelet."""
+    monkeypatch.setenv("BDPT_LDS_MODE", lds)
+    W, H, S, M = 384, 216, 2, 8
+    sc = _with_env(_standin(W, H), 256, 128)
+    g = _gpu_render(sc, W, H, S, M, rr=True)
+    _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32, rr=True), f"stand-in + env + RR m8 LM {lds}")
+
+
+@pytest.mark.parametrize("env", [{"BDPT_XCD_GROUPS": "1"}, {"BDPT_BLOCK_MAJOR": "0"},
+                                 {"BDPT_XCD_GROUPS": "1", "BDPT_BLOCK_MAJOR": "0"}])
+def test_ticket_orders(env, monkeypatch):
+    """The work-item orders kept as A/B switches (XCD-grouped tickets with their per-group counters
+    and exhaustion hand-over; chunk-major order) render the same image."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    W, H, S, M = 200, 150, 5, 5      # 5 spp: a ragged last chunk of the 2-sample work items
+    sc = _standin(W, H)
+    _check_frames(_gpu_render(sc, W, H, S, M), oracle_render(sc, W, H, S, M, MODE_C32), f"tickets {env}")
+
+
+def test_concurrent_tile_callers():
+    """The reference's caller model: N host threads drive raytrace_tile (and raytrace_pixel) on
+    one PathTracer (raytraced_renderer.cpp:325-327,610-615). The ctx serialises the calls; the image
+    equals one full-frame render."""
+    import threading
+    W, H, S, M = 160, 120, 2, 5
+    sc = golden_scene("CBgems", W, H)
+    full = _gpu_render(sc, W, H, S, M)
+    pt = B.BidirectionalPathTracer(sc, W, H, S, M)
+    try:
+        tiles = [(x, y, 32, 32) for y in range(0, H, 32) for x in range(0, W, 32)]
+        todo = list(tiles)
+        lock = threading.Lock()
+        errs = []
+
+        def worker():
+            try:
+                while True:
+                    with lock:
+                        if not todo:
+                            return
+                        t = todo.pop()
+                    pt.raytrace_tile(*t)
+            except Exception as e:   # pragma: no cover - reported below
+                errs.append(e)
+        th = [threading.Thread(target=worker) for _ in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs
+        got = pt.read_frame(B.FRAME_SAMPLE).astype(np.float64)
+    finally:
+        pt.close()
+    assert _rmse(got, full["sample"]) < 1e-6
+    # 1x1 tiles (raytrace_pixel) back to back: the staging ring never waits for the GPU
+    pt = B.BidirectionalPathTracer(sc, W, H, S, M)
+    try:
+        for x in range(8):
+            pt.raytrace_pixel(40 + x, 60)
+        eye = pt.read_frame(B.FRAME_EYE).astype(np.float64)
+    finally:
+        pt.close()
+    assert _rmse(eye[60, 40:48], full["eye"][60, 40:48]) < RMSE_TOL
+    assert np.count_nonzero(eye.sum(axis=2)) <= 8

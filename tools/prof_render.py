@@ -16,8 +16,7 @@ W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (480, 360)
 spp = int(sys.argv[4]) if len(sys.argv) > 4 else 128
 M = int(sys.argv[5]) if len(sys.argv) > 5 else 5
 launches = int(sys.argv[6]) if len(sys.argv) > 6 else 2
-if os.environ.get("BDPT_LIB"):
-    B.load_library(os.environ["BDPT_LIB"])
+if os.environ.get("BDPT_LIB"):   # a variant build replaces the default library (loaded once)
     B._lib = B.load_library(os.environ["BDPT_LIB"])
 sc = B.load_dae(scene, W, H) if scene.endswith(".dae") else golden_scene(scene, W, H)
 pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489, samples_per_lane=int(os.environ.get("BDPT_SPL", "0")),
