@@ -1188,13 +1188,11 @@ BDPT_HD float step_gx(f3 cur_pos, f3 cur_n, bool cur_env, f3 oth_pos, f3 oth_zh,
 }
 BDPT_HD bool is_env(const Vtx& v) { return v.mat == MAT_ENV_V; }
 
-// Non-EXT walks compute each vertex's MIS constants when the vertex is created (prepare_sample);
-// the two passes below then run only for EXT kernels.
+// The walk computes each vertex's MIS constants when the vertex is created (prepare_sample,
+// BDPT_FUSED_CONSTANTS); the two passes below are the reference-shaped form of the same values,
+// kept for BDPT_FUSED_CONSTANTS=0 A/B builds.
 #ifndef BDPT_FUSED_CONSTANTS
 #define BDPT_FUSED_CONSTANTS 1
-#endif
-#ifndef BDPT_FUSED_REGS
-#define BDPT_FUSED_REGS 1   // previous vertex from registers (measured +1% over re-reading it from scratch)
 #endif
 // Per-subpath MIS constants (see Vtx). EXT: the scene has an environment light or the walks use
 // Russian roulette (q = Vtx::gp on entry); EXT = false compiles to the reference-only path.
@@ -1569,7 +1567,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.alpha = divs(lrad, lpp);
     v1.mat = l1env ? (int)MAT_ENV_V : -1;
     v1.gp = 0; v1.cq = 0;
-    v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused non-EXT walk)
+    v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused walk)
   }
   P.l1_dir_pdf = mis_dir;
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
@@ -1581,9 +1579,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   int i = 2, count = 0;
   uint32_t dm = 0;
   bool light = false;
-#if BDPT_FUSED_CONSTANTS && BDPT_FUSED_REGS
-  int pv_mat = -1;          // the previous vertex's material / fwd / prefix (fused constants)
-  float pv_fwd = 1.0f, pv_gp = 0.0f;
+#if BDPT_FUSED_CONSTANTS
+  // the previous vertex's material / fwd / prefix / roulette probability (fused constants)
+  int pv_mat = -1;
+  float pv_fwd = 1.0f, pv_gp = 0.0f, pv_q = 1.0f;
 #endif
   for (;;) {
     Hit h;
@@ -1603,6 +1602,12 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.zh = v.n;
       v.mat = MAT_ENV_V;
       v.fwd = 1; v.gp = 1; v.cq = 0;
+#if BDPT_FUSED_CONSTANTS
+      // eye_constants of an env vertex: g = 1 toward it, the previous vertex's BSDF density of rd
+      // times its roulette probability; no prefix (the j = 0 weight recomputes this step)
+      if (count > 0) v.fwd = pdf_b(S.mats[pv_mat], prev_n, zaxis(prev_n), rd) * pv_q * 1.0f;
+      v.gp = 0.0f;
+#endif
       P.E[count++] = v;
     }
     if (!end) {
@@ -1622,41 +1627,46 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       Vtx* slot = (light ? P.L + 1 : P.E) + count++;
       if (is_delta(M.type)) dm |= 1u << i;
 #if BDPT_FUSED_CONSTANTS
-      if (!EXT) {
-        // eye_constants / light_constants of this vertex at its creation: the previous vertex is the
-        // one just below it on the same subpath (camera: no step; light vertex L[1] for the light's
-        // first hit), so nothing is re-read after the walk
-        const bool conn = M.type == MAT_DIFFUSE && lz(normalize(sub(ro, v.pos)), v.zh) >= 0 && nonzero3(v.alpha);
-        v.cq = conn ? 1.0f : 0.0f;
-        if (!light && count == 1) {
-          v.fwd = 1.0f * 1.0f;
-          v.gp = 0.0f;
-        } else {
-#if BDPT_FUSED_REGS
-          // the previous vertex from the walk's registers: position ro, normal prev_n (its shading
-          // axis is normalize(prev_n), as make_frame / zaxis compute it), material, fwd, prefix
-          Vtx nx;
-          nx.pos = ro; nx.n = prev_n; nx.zh = zaxis(prev_n);
-          nx.mat = pv_mat; nx.fwd = pv_fwd; nx.gp = pv_gp;
-#else
-          const Vtx nx = light ? P.L[count - 1] : P.E[count - 2];
-#endif
-          f3 dw;
-          const float g2 = step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
-          const float p = (light && count == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw);
-          v.fwd = p * g2;
-          const float g = step_g(nx.pos, nx.n, v.pos, v.zh, &dw);
-          const float pp = pdf_b(M, v.n, v.zh, dw);
-          v.gp = mis_horner((pp * g) / nx.fwd, !((dm >> (i - 2)) & 3u), nx.gp);
-        }
-#if BDPT_FUSED_REGS
-        pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp;
-#endif
+      // eye_constants / light_constants of this vertex at its creation. The previous vertex is the
+      // one just below it on the same subpath (camera: no step; the light vertex L[1] for the
+      // light's first hit) and is still in registers: position ro, normal prev_n (shading axis
+      // normalize(prev_n), as make_frame / zaxis compute it; an environment L[1] keeps n itself),
+      // material, fwd, prefix, roulette probability. The prefix and the connectability need this
+      // vertex's own roulette probability, known after its sample_f below (EXT), so they are
+      // finished there: gp = horner(((pp * q) * g) / fwd_prev, t, gp_prev), cq = conn ? q : 0.
+      const bool conn = M.type == MAT_DIFFUSE && lz(normalize(sub(ro, v.pos)), v.zh) >= 0 && nonzero3(v.alpha);
+      const bool first_eye = !light && count == 1;
+      float gp_pp = 0.0f, gp_g = 0.0f;
+      if (first_eye) {
+        v.fwd = 1.0f * 1.0f;
+      } else {
+        const bool nx_env = EXT && light && count == 1 && l1env;
+        const f3 nx_zh = nx_env ? prev_n : zaxis(prev_n);
+        f3 dw;
+        const float g2 = EXT ? step_gx(v.pos, v.n, false, ro, nx_zh, nx_env, &dw) : step_g(v.pos, v.n, ro, nx_zh, &dw);
+        const float p = (light && count == 1) ? P.l1_dir_pdf
+                                              : pdf_b(S.mats[pv_mat], prev_n, nx_zh, dw) * (EXT ? pv_q : 1.0f);
+        v.fwd = p * g2;
+        gp_g = EXT ? step_gx(ro, prev_n, nx_env, v.pos, v.zh, false, &dw) : step_g(ro, prev_n, v.pos, v.zh, &dw);
+        gp_pp = pdf_b(M, v.n, v.zh, dw);
       }
+      const bool gp_t = !((dm >> (i - 2)) & 3u);
+      auto finish = [&](float q) {   // q: this vertex's roulette probability (1 without roulette)
+        v.cq = conn ? (EXT ? q : 1.0f) : 0.0f;
+        v.gp = first_eye ? 0.0f : mis_horner(((EXT ? gp_pp * q : gp_pp) * gp_g) / pv_fwd, gp_t, pv_gp);
+        pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp; pv_q = q;
+      };
+      if (!EXT) finish(1.0f);
 #endif
       *slot = v;
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
+#if BDPT_FUSED_CONSTANTS
+        if (EXT) {
+          finish(1.0f);
+          slot->gp = v.gp; slot->cq = v.cq;
+        }
+#endif
       } else {
         f3 wi;
         float pdf;
@@ -1668,6 +1678,12 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
           slot->gp = q;
           if (!(rng_next(g) < q)) end = true;
         }
+#if BDPT_FUSED_CONSTANTS
+        if (EXT) {
+          finish(q);
+          slot->gp = v.gp; slot->cq = v.cq;
+        }
+#endif
         ro = hit_p;
         rd = normalize(to_world(fr, wi));
         rmin = BDPT_EPS_F;
@@ -1696,12 +1712,12 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       prev_f = splat3(1.0f);
       prev_n = ln;
       i = 2; count = 0; dm = 0;
-#if BDPT_FUSED_CONSTANTS && BDPT_FUSED_REGS
-      pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f;   // the light vertex L[1]
+#if BDPT_FUSED_CONSTANTS
+      pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
 #endif
     }
   }
-  if (EXT || !BDPT_FUSED_CONSTANTS) {
+  if (!BDPT_FUSED_CONSTANTS) {
     eye_constants<MAXV, EXT>(S, P);
     light_constants<MAXV, EXT>(S, P, mis_p);
   }

@@ -118,6 +118,8 @@ struct SahBuilder {
   // 63.3 -> 26.2 (large wall triangles no longer share leaves with the mesh).
   int leaf_max = 2;
   double ct = 1.0;
+  int nb = 16;          // centroid bins per axis (<= kMaxBins)
+  static constexpr int kMaxBins = 64;
   static double area(const Box& b) {
     const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
     return dx < 0 ? 0 : 2 * (dx * dy + dy * dz + dz * dx);
@@ -142,14 +144,14 @@ struct SahBuilder {
       double c[3] = {B[prims[i]].centroid(0), B[prims[i]].centroid(1), B[prims[i]].centroid(2)};
       cb.expand_pt(c);
     }
-    constexpr int NB = 16;
+    const int NB = nb;
     double best = INFINITY;
     int best_axis = -1, best_split = 0;
     for (int ax = 0; ax < 3; ax++) {
       const double lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
       if (!(ext > 0)) continue;
-      Box bb[NB];
-      int cnt[NB] = {0};
+      Box bb[kMaxBins];
+      int cnt[kMaxBins] = {0};
       for (int b = 0; b < NB; b++)
         for (int k = 0; k < 3; k++) { bb[b].mn[k] = INFINITY; bb[b].mx[k] = -INFINITY; }
       for (int i = 0; i < n; i++) {
@@ -158,8 +160,8 @@ struct SahBuilder {
         cnt[b]++;
         bb[b].expand(B[prims[i]]);
       }
-      double ra[NB];
-      int rc[NB];
+      double ra[kMaxBins];
+      int rc[kMaxBins];
       Box acc;
       for (int k = 0; k < 3; k++) { acc.mn[k] = INFINITY; acc.mx[k] = -INFINITY; }
       int c = 0;
@@ -398,6 +400,7 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
     // diagnostics / A-B: leaf size and SAH termination of the device tree (no effect on results)
     if (const char* e = getenv("BDPT_SAH_LEAF")) S.leaf_max = std::max(1, std::min(4, atoi(e)));
     if (const char* e = getenv("BDPT_SAH_CT")) S.ct = atof(e);
+    if (const char* e = getenv("BDPT_SAH_BINS")) S.nb = std::max(2, std::min(SahBuilder::kMaxBins, atoi(e)));
     std::vector<int> idx(n);
     for (int i = 0; i < n; i++) idx[i] = i;
     root = S.build(idx.data(), n, 0);
