@@ -128,6 +128,19 @@ class Scene:
         e.rgb = self.envmap.ctypes.data_as(C.POINTER(C.c_float))
         self._env_desc = e
 
+    def load_camera(self, path: str) -> None:
+        """Application::load_camera -> Camera::load_settings (application.h:114-116, camera.cpp:172-186):
+        the -c camera-settings file through bdpt_camera_load_settings (w2c kept, as the reference
+        does not recompute it)."""
+        lib = load_library()
+        cam = self.desc().camera
+        _check(lib.bdpt_camera_load_settings(os.fsencode(path), C.byref(cam)), lib)
+        c = dict(self.camera)
+        c["pos"] = list(cam.pos)
+        c["c2w_cols"] = [list(cam.c2w[3 * k:3 * k + 3]) for k in range(3)]
+        c["hFov"], c["vFov"], c["nClip"], c["fClip"] = cam.hfov_deg, cam.vfov_deg, cam.nclip, cam.fclip
+        self.camera = c
+
     @property
     def nprim(self) -> int:
         return int(self.prim_type.shape[0])
@@ -308,6 +321,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_dae_get_desc.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
     lib.bdpt_dae_dump_json.argtypes = [C.c_void_p, C.c_char_p]
     lib.bdpt_dae_free.argtypes = [C.c_void_p]
+    lib.bdpt_camera_load_settings.argtypes = [C.c_char_p, C.POINTER(Camera)]
     lib.bdpt_dae_free.restype = None
     lib.bdpt_exr_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                   C.POINTER(C.POINTER(C.c_float))]

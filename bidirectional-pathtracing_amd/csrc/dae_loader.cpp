@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <map>
 #include <memory>
 #include <set>
@@ -255,7 +256,7 @@ struct Parser {
     XEl* e = x;
     while (e && std::getline(ss, tok, '/')) e = e->first(tok.c_str());
     if (e) {
-      if (const char* url = e->attr("url")) e = uri_find(url + 1);
+      if (const char* url = e->attr("url")) e = uri_find(url_id(url));
     }
     return e;
   }
@@ -365,7 +366,7 @@ struct Parser {
         if (XEl* im = get(x, "instance_geometry/bind_material/technique_common/instance_material")) {
           const char* tg = im->attr("target");
           if (!tg) { err = "instance_material without target"; return false; }
-          XEl* m = uri_find(tg + 1);
+          XEl* m = uri_find(url_id(tg));
           if (!m) { err = std::string("unknown material ") + tg; return false; }
           if (!parse_material(m, node.mat)) return false;
           node.has_mat = true;
@@ -432,6 +433,9 @@ struct Parser {
     return true;
   }
 
+  // "#id" of a source / url attribute ("" when absent)
+  static std::string url_id(const char* a) { return !a ? std::string() : std::string(a[0] == '#' ? a + 1 : a); }
+
   bool parse_mesh(XEl* x, Node& n) {
     XEl* m = x->first("mesh");
     if (!m) { err = "geometry without mesh"; return false; }
@@ -442,7 +446,7 @@ struct Parser {
       const char* cnt = fa->attr("count");
       size_t nf = cnt ? (size_t)atol(cnt) : 0;
       std::vector<float> f;
-      f.reserve(nf);
+      f.reserve(std::min(nf, fa->text.size() / 2 + 1));   // a count beyond the text reads what is there
       const char* p = fa->text.c_str();
       for (size_t i = 0; i < nf; i++) {
         char* end;
@@ -461,7 +465,7 @@ struct Parser {
     for (XEl* in = ev->first("input"); in; in = in->next("input")) {
       const char* sem = in->attr("semantic");
       if (!sem || std::string(sem) != "POSITION") continue;
-      auto it = src.find(in->attr("source") + 1);
+      auto it = src.find(url_id(in->attr("source")));
       if (it == src.end()) { err = "bad POSITION source"; return false; }
       for (size_t i = 0; i + 2 < it->second.size(); i += 3)
         verts.emplace_back(it->second[i], it->second[i + 1], it->second[i + 2]);
@@ -477,7 +481,7 @@ struct Parser {
       if (sem == "VERTEX") {
         hv = true;
         vo = off;
-        if (std::string(in->attr("source") + 1) != vid) { err = "VERTEX source mismatch"; return false; }
+        if (url_id(in->attr("source")) != vid) { err = "VERTEX source mismatch"; return false; }
         n.verts = verts;
       }
       if (sem == "NORMAL") hn = true;
@@ -491,15 +495,20 @@ struct Parser {
     std::vector<size_t> sizes;
     size_t nidx = 0;
     {
+      // malformed files (counts beyond the lists, offsets beyond the stride) are rejected here;
+      // the reference's parser would read past its arrays on them
       const char* p = vc->text.c_str();
       for (size_t i = 0; i < npoly; i++) {
         char* end;
         size_t s = strtoul(p, &end, 10);
+        if (end == p || s > pp->text.size()) { err = "polylist vcount does not match its count"; return false; }
         p = end;
         sizes.push_back(s);
         nidx += s * stride;
       }
     }
+    if (hv && vo >= stride) { err = "polylist input offset beyond its stride"; return false; }
+    if (nidx > pp->text.size()) { err = "polylist p shorter than its vcount"; return false; }
     std::vector<size_t> idx;
     idx.reserve(nidx);
     {
@@ -507,6 +516,7 @@ struct Parser {
       for (size_t i = 0; i < nidx; i++) {
         char* end;
         size_t v = strtoul(p, &end, 10);
+        if (end == p) { err = "polylist p shorter than its vcount"; return false; }
         p = end;
         idx.push_back(v);
       }
@@ -1079,5 +1089,35 @@ int bdpt_dae_dump_json(const bdpt_dae* d, const char* path) {
 }
 
 void bdpt_dae_free(bdpt_dae* d) { delete d; }
+
+int bdpt_camera_load_settings(const char* path, bdpt_camera* cam) {
+  if (!path || !cam) { bdpt::g_err = "null argument"; return BDPT_E_INVALID; }
+  std::ifstream file(path);
+  if (!file.is_open()) { bdpt::g_err = std::string("cannot open camera settings ") + path; return BDPT_E_INVALID; }
+  // Camera::load_settings (camera.cpp:172-186): the same extractions into the same types, so a
+  // short or malformed file leaves / zeroes the same members the reference's would
+  double hFov = cam->hfov_deg, vFov = cam->vfov_deg, ar = 0, nClip = cam->nclip, fClip = cam->fclip;
+  double pos[3] = {cam->pos[0], cam->pos[1], cam->pos[2]}, target[3] = {0, 0, 0};
+  double phi = 0, theta = 0, r = 0, minR = 0, maxR = 0;
+  double c2w[3][3];   // (row, col)
+  for (int i = 0; i < 9; ++i) c2w[i / 3][i % 3] = cam->c2w[3 * (i % 3) + i / 3];
+  size_t screenW = 0, screenH = 0;
+  double screenDist = 0, focalDistance = 0, lensRadius = 0;
+  file >> hFov >> vFov >> ar >> nClip >> fClip;
+  for (int i = 0; i < 3; ++i) file >> pos[i];
+  for (int i = 0; i < 3; ++i) file >> target[i];
+  file >> phi >> theta >> r >> minR >> maxR;
+  for (int i = 0; i < 9; ++i) file >> c2w[i / 3][i % 3];
+  file >> screenW >> screenH >> screenDist;
+  file >> focalDistance >> lensRadius;
+  cam->hfov_deg = hFov;
+  cam->vfov_deg = vFov;
+  cam->nclip = nClip;
+  cam->fclip = fClip;
+  for (int i = 0; i < 3; ++i) cam->pos[i] = pos[i];
+  for (int i = 0; i < 9; ++i) cam->c2w[3 * (i % 3) + i / 3] = c2w[i / 3][i % 3];   // column-major
+  fprintf(stderr, "[Camera] Loaded settings from %s\n", path);
+  return BDPT_OK;
+}
 
 }  // extern "C"

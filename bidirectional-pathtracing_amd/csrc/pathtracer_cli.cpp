@@ -1,7 +1,7 @@
 // pathtracer_cli.cpp — the reference's `pathtracer` command line (src/application/main.cpp:62-200)
 // in windowless mode, rendering through libbdpt_amd.so on MI355X GPUs.
 //
-//   pathtracer [-s spp] [-m max_depth] [-r W H] [-f out.png] [-p x y dx dy] [-t threads]
+//   pathtracer [-s spp] [-m max_depth] [-r W H] [-f out.png] [-p x y dx dy] [-t threads] [-c cam.txt]
 //              [-l n] [-e envmap.exr] [--rr] [-g gpus] [-S seed] [--dump-scene scene.json]
 //              [--pt [-a batch tol] [-H] [-b lens] [-d focal]] scene.dae
 //
@@ -41,6 +41,7 @@ void usage(const char* b) {
   printf("  -d  <FLOAT>      PathTracer: focal distance\n");
   printf("  -e  <PATH>       Path to environment map\n");
   printf("  --rr             Russian roulette on both subpaths\n");
+  printf("  -c  <FILENAME>   Load camera settings file (Camera::dump_settings format)\n");
   printf("  -f  <FILENAME>   Image (.png) file to save output to\n");
   printf("  -r  <INT> <INT>  Width and height of output image\n");
   printf("  -p  <x> <y> <dx> <dy>  Render only this cell\n");
@@ -63,7 +64,7 @@ int main(int argc, char** argv) {
   int spp = 1, max_depth = 1, w = 0, h = 0, gpus = 1;
   long cx = -1, cy = 0, cdx = 0, cdy = 0;
   unsigned long long seed = 5489;
-  std::string out, dump, scene, envpath;
+  std::string out, dump, scene, envpath, cam_settings;
   bool rr = false, pt = false, hemi = false;
   int nal = 1, batch = 32;
   float tol = 0.05f;
@@ -104,10 +105,8 @@ int main(int argc, char** argv) {
       if (!bdpt::write_png(o, bdpt::tonemap(hdr.data(), tw, tht), tw, tht)) return 1;
       return bdpt::write_rate_png(o, std::vector<float>((size_t)tw * tht, 1.0f), tw, tht) ? 0 : 1;
     }
-    else if (a == "-c") {
-      fprintf(stderr, "[PathTracer] option %s is not supported by the BDPT GPU path\n", a.c_str());
-      return 1;
-    } else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
+    else if (a == "-c") { need(1); cam_settings = argv[++i]; }
+    else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
     else scene = a;
   }
   if (scene.empty()) { usage(argv[0]); return 1; }
@@ -123,6 +122,9 @@ int main(int argc, char** argv) {
   if (w <= 0 || h <= 0) { w = 800; h = 600; }
   bdpt_scene_desc desc;
   bdpt_dae_get_desc(dae, &desc);
+  // -c: after the -r resize, before rendering (main.cpp:172-178)
+  if (!cam_settings.empty() && bdpt_camera_load_settings(cam_settings.c_str(), &desc.camera) != BDPT_OK)
+    fprintf(stderr, "[PathTracer] %s (camera unchanged)\n", bdpt_last_error());
   bdpt_envmap env;
   float* env_rgb = nullptr;
   if (!envpath.empty()) {

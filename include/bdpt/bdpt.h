@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 4
+#define BDPT_ABI_VERSION 5
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -247,6 +247,17 @@ int bdpt_dae_get_desc(const bdpt_dae* scene, bdpt_scene_desc* out);
 /* Writes the scene in the JSON dump format of tests/golden/scenes (round-trip doubles). */
 int bdpt_dae_dump_json(const bdpt_dae* scene, const char* path);
 void bdpt_dae_free(bdpt_dae* scene);
+
+/* ABI v5: the CLI's -c camera-settings file (main.cpp:120-121,177-178 -> Application::load_camera
+ * -> Camera::load_settings, camera.cpp:172-186), read with the reference's stream extraction order
+ * (hFov vFov ar nClip fClip, pos, targetPos, phi theta r minR maxR, c2w row by row, screenW
+ * screenH screenDist, focalDistance lensRadius: the format Camera::dump_settings writes). It
+ * replaces cam's hfov_deg, vfov_deg, nclip, fclip, pos and c2w. w2c is kept: load_settings does
+ * not recompute it (w2c = c2w.inv() only happens in compute_position, camera.cpp:146), so the
+ * reference's t = 1 camera connections keep using the placement's inverse — reproduced here.
+ * A file that cannot be opened leaves cam unchanged (as the reference's ifstream does) and returns
+ * BDPT_E_INVALID. */
+int bdpt_camera_load_settings(const char* path, bdpt_camera* cam);
 
 /* Host-side OpenEXR reader for the -e environment map (main.cpp:40-77 load_exr, tinyexr):
  * scanline files with NONE / RLE / ZIPS / ZIP compression and HALF / FLOAT / UINT channels.

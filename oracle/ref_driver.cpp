@@ -242,11 +242,11 @@ int main(int argc, char** argv) {
   float tol = 0.05f;
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
-  std::string png = "/dev/null", npy_prefix, scene_json;
+  std::string png = "/dev/null", npy_prefix, scene_json, cam_settings;
   bool render = true, uni = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -263,6 +263,7 @@ int main(int argc, char** argv) {
       case 'b': lens = atof(optarg); break;              // main.cpp:128-130
       case 'd': focal = atof(optarg); break;             // main.cpp:131-133
       case 'a': batch = atoi(argv[optind - 1]); tol = atof(argv[optind]); optind++; break;   // main.cpp:134-137
+      case 'c': cam_settings = optarg; break;            // main.cpp:120-121
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -333,6 +334,8 @@ int main(int argc, char** argv) {
   }
   // --- main.cpp:172-173 -> Application::resize (application.cpp:188-200) ---
   if (w && h) { screenW = w; screenH = h; camera.set_screen_size(w, h); }
+  // --- main.cpp:177-178 -> Application::load_camera (application.h:114-116) ---
+  if (!cam_settings.empty()) camera.load_settings(cam_settings);
 
   // --- Application ctor (application.cpp:21-40) with AppConfig defaults (application.h:45-65) ---
   RaytracedRenderer* rr = new RaytracedRenderer(ns_aa, max_depth, nal, 1, 1, 1, threads, batch, tol,
