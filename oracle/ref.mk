@@ -47,6 +47,21 @@ $(OUT)/obj/ref_driver.o: oracle/ref_driver.cpp
 $(OUT)/ref_driver: $(OBJS) $(OUT)/obj/glew.o $(OUT)/obj/ref_driver.o
 	$(CXX) -o $@ $^ -lGL -lpthread
 
+# integration check (tests/test_integration.py): ref_driver with the reference-side binding
+# integration/bidirection_amd.h swapped in for BidirectionalPathTracer (-G), linked to the product
+# library. `make -f oracle/ref.mk amd` after libbdpt_amd.so is built.
+LIBDIR := bidirectional-pathtracing_amd
+$(OUT)/obj/ref_driver_amd.o: oracle/ref_driver.cpp integration/bidirection_amd.h include/bdpt/bdpt.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -DBDPT_INTEGRATION -Iinclude -Iintegration -c $< -o $@
+
+$(OUT)/ref_driver_amd: $(OBJS) $(OUT)/obj/glew.o $(OUT)/obj/ref_driver_amd.o $(LIBDIR)/libbdpt_amd.so
+	$(CXX) -o $@ $(OBJS) $(OUT)/obj/glew.o $(OUT)/obj/ref_driver_amd.o -L$(LIBDIR) -l:libbdpt_amd.so \
+	  -L/opt/rocm/lib -Wl,-rpath-link,/opt/rocm/lib -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lGL -lpthread
+
+amd: $(OUT)/ref_driver_amd
+.PHONY: all amd
+
 # environment-light known answers (tests/test_env.py): EnvironmentLight + sampler + tinyexr
 ENV_OBJS := $(addprefix $(OUT)/obj/,src/scene/environment_light.o src/pathtracer/sampler.o CGL/src/lodepng.o \
             CGL/src/vector2D.o CGL/src/vector3D.o CGL/src/vector4D.o CGL/src/matrix3x3.o CGL/src/matrix4x4.o \

@@ -58,6 +58,9 @@
 #include "scene/gl_scene/ambient_light.h"
 #include "scene/gl_scene/spot_light.h"
 #include "scene/scene.h"
+#ifdef BDPT_INTEGRATION
+#include "bidirection_amd.h"   // integration/: the reference-side binding to libbdpt_amd.so
+#endif
 #include "scene/light.h"
 #include "scene/triangle.h"
 #include "scene/sphere.h"
@@ -243,10 +246,10 @@ int main(int argc, char** argv) {
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
   std::string png = "/dev/null", npy_prefix, scene_json, cam_settings;
-  bool render = true, uni = false;
+  bool render = true, uni = false, amd = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:G")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -264,6 +267,7 @@ int main(int argc, char** argv) {
       case 'd': focal = atof(optarg); break;             // main.cpp:131-133
       case 'a': batch = atoi(argv[optind - 1]); tol = atof(argv[optind]); optind++; break;   // main.cpp:134-137
       case 'c': cam_settings = optarg; break;            // main.cpp:120-121
+      case 'G': amd = true; break;                       // integration check (BDPT_INTEGRATION builds)
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -355,6 +359,36 @@ int main(int argc, char** argv) {
   rr->set_frame_size(screenW, screenH);
   if (!scene_json.empty()) dump_scene(scene_json, rr, camera);
   if (!render) return 0;
+  if (amd) {
+#ifdef BDPT_INTEGRATION
+    // integration/bidirection_amd.h in place of the reference's BidirectionalPathTracer: the
+    // primitives in build_accel's collection order (raytraced_renderer.cpp:352-360), the scene's
+    // lights (the env light appended last, :117-119) and the camera, then one whole-frame render
+    // through libbdpt_amd.so; -o writes its sampleBuffer like the reference path does.
+    BidirectionalPathTracerAMD gpu;
+    gpu.ns_aa = rr->pt->ns_aa;
+    gpu.max_ray_depth = rr->pt->max_ray_depth;
+    gpu.set_frame_size(screenW, screenH);
+    std::vector<SceneObjects::Primitive*> prims;
+    for (SceneObjects::SceneObject* obj : rr->scene->objects) {
+      const std::vector<SceneObjects::Primitive*>& op = obj->get_primitives();
+      prims.insert(prims.end(), op.begin(), op.end());
+    }
+    const int rc = gpu.attach(prims, rr->scene->lights, camera, envmap);
+    if (rc != BDPT_OK) {
+      fprintf(stderr, "[ref_driver] BidirectionalPathTracerAMD::attach: %d (%s)\n", rc, bdpt_last_error());
+      return 20 - rc;   // BDPT_E_DEVICE (-3) -> 23
+    }
+    gpu.raytrace_frame();
+    gpu.finish();
+    if (!npy_prefix.empty()) write_npy(npy_prefix + "_sample.npy", gpu.sampleBuffer);
+    fprintf(stdout, "[ref_driver] rendered through libbdpt_amd.so\n");
+    return 0;
+#else
+    fprintf(stderr, "[ref_driver] -G needs the BDPT_INTEGRATION build (oracle/_ref/ref_driver_amd)\n");
+    return 2;
+#endif
+  }
   rr->render_to_file(png, (size_t)-1, 0, 0, 0);
   if (!npy_prefix.empty() && uni) {
     write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);
