@@ -46,6 +46,7 @@ void usage(const char* b) {
   printf("  -r  <INT> <INT>  Width and height of output image\n");
   printf("  -p  <x> <y> <dx> <dy>  Render only this cell\n");
   printf("  -g  <INT>        Number of GPUs (default 1)\n");
+  printf("  --devices <LIST> Device of each of the -g workers, comma-separated (default 0..N-1)\n");
   printf("  -S  <INT>        RNG seed (default 5489)\n");
   printf("  --dump-scene <FILE>  Write the loaded scene as JSON\n");
   printf("  --tonemap <in.f64> <W> <H> <out.png>  Output stage only: raw float64 RGB (row 0 =\n"
@@ -65,6 +66,7 @@ int main(int argc, char** argv) {
   long cx = -1, cy = 0, cdx = 0, cdy = 0;
   unsigned long long seed = 5489;
   std::string out, dump, scene, envpath, cam_settings;
+  std::vector<int> devices;
   bool rr = false, pt = false, hemi = false;
   int nal = 1, batch = 32;
   float tol = 0.05f;
@@ -87,6 +89,16 @@ int main(int argc, char** argv) {
     else if (a == "-r") { need(2); w = atoi(argv[i + 1]); h = atoi(argv[i + 2]); i += 2; }
     else if (a == "-p") { need(4); cx = atol(argv[i + 1]); cy = atol(argv[i + 2]); cdx = atol(argv[i + 3]); cdy = atol(argv[i + 4]); i += 4; }
     else if (a == "-g") { need(1); gpus = atoi(argv[++i]); }
+    else if (a == "--devices") {   // device of each -g worker (default 0..N-1), e.g. 0,0 on a one-GPU box
+      need(1);
+      devices.clear();
+      for (const char* q = argv[++i]; *q;) {
+        char* end;
+        devices.push_back((int)strtol(q, &end, 10));
+        if (end == q) break;
+        q = *end == ',' ? end + 1 : end;
+      }
+    }
     else if (a == "-S") { need(1); seed = strtoull(argv[++i], nullptr, 10); }
     else if (a == "--dump-scene") { need(1); dump = argv[++i]; }
     else if (a == "-e") { need(1); envpath = argv[++i]; }
@@ -109,7 +121,7 @@ int main(int argc, char** argv) {
     else if (a == "-h" || (a.size() > 1 && a[0] == '-')) { usage(argv[0]); return 1; }
     else scene = a;
   }
-  if (scene.empty()) { usage(argv[0]); return 1; }
+  if (scene.empty() || gpus < 1) { usage(argv[0]); return 1; }
   fprintf(stderr, "[PathTracer] Input scene file: %s\n", scene.c_str());
   bdpt_dae* dae = nullptr;
   if (bdpt_dae_load(scene.c_str(), w, h, &dae) != BDPT_OK) return fail("loading scene");
@@ -148,7 +160,8 @@ int main(int argc, char** argv) {
     th.emplace_back([&, g] {
       bdpt_params p;
       memset(&p, 0, sizeof p);
-      p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed; p.device = g;
+      p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed;
+      p.device = g < (int)devices.size() ? devices[g] : g;
       p.russian_roulette = rr ? 1 : 0;
       if (pt) {
         p.integrator = BDPT_INTEGRATOR_PT;

@@ -93,3 +93,24 @@ def test_cli_pathtracer(tmp_path, scene):
     d = np.abs(ours.astype(int) - ref.astype(int))
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
     assert os.path.exists(tmp_path / "pt_rate.png")   # sampleCountBuffer / ns_aa, as save_sampling_rate_image
+
+
+@pytest.mark.parametrize("gpus,spp", [(2, 2), (3, 4)])
+def test_cli_multi_gpu_split(tmp_path, gpus, spp):
+    """-g N: the sample range split over N workers (one context and one host thread each) and the
+    frames summed on the host. --devices puts every worker on device 0 so a one-GPU box runs the
+    N-worker path; the image must match one render of all samples (oracle mode 2)."""
+    W, H, M = 64, 48, 5
+    out = tmp_path / "g.png"
+    r = subprocess.run([CLI, "-s", str(spp), "-m", str(M), "-r", str(W), str(H), "-g", str(gpus), "--devices",
+                        ",".join(["0"] * gpus), "-f", str(out), os.path.join(REPO, "scenes", "CBspheres.dae")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"{gpus} GPU(s)" in r.stderr
+    ours = read_png(out)
+    ref_hdr = oracle_render(golden_scene("CBspheres", W, H), W, H, spp, M, MODE_C32)[0]
+    raw = tmp_path / "ref.f64"
+    np.ascontiguousarray(ref_hdr, dtype="<f8").tofile(raw)
+    subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
+    d = np.abs(ours.astype(int) - read_png(tmp_path / "ref.png").astype(int))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
