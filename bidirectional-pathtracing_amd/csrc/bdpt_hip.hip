@@ -49,6 +49,7 @@ struct KParams {
   int xcd;                    // 1: blocks b, b+8, ... (one XCD) take items from their own eighth first
   int n_node4, n_geom4;       // float4 counts of the node / geometry arrays (LDS staging)
   int nmat;
+  unsigned item_lo;           // first item of this launch (tickets count from it)
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -274,17 +275,17 @@ constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLig
 constexpr size_t kStaticLds = 0;
 #endif
 
-// LM (LDS mode): 0 = scene read from HBM/L2; 1 = whole BVH + geometry staged in LDS by every
-// block; 2 = the top n_top BFS-ordered nodes (the part every ray traverses) staged in LDS.
-// EXT: environment light and/or Russian roulette (DESIGN.md §9); EXT = false is the reference-only
-// path with no trace of either in the generated code.
-template <int MAXV, bool STATS, int LM, bool EXT>
-__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
-  // One dynamic LDS array: [wave queues][optional scene / treelet copy]
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  WaveQ* qs = (WaveQ*)smem;
-  const int lane = threadIdx.x & 63;
-  WaveQ& q = qs[threadIdx.x >> 6];
+#ifdef BDPT_PHASE_PROF
+#define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define PH_STAMP(v)
+#endif
+
+// Stages the block's LDS copy of the scene (LM 1: whole tree + geometry; LM 2: the BFS treelet;
+// LM 3: the flat leaf list with its geometry and shading records) behind the wave queues, and the
+// materials / lights, and points kp.S at them.
+template <int LM>
+__device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DMat* s_mats, DLight* s_lights) {
   if (LM != 0) {
     float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
     const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
@@ -304,8 +305,6 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     kp.S.lgeom = sc + nn;
   }
 #if BDPT_MATS_LDS
-  __shared__ DMat s_mats[kLdsMats];
-  __shared__ DLight s_lights[kLdsLights];
   if (kp.nmat <= kLdsMats && kp.S.nlights <= kLdsLights) {
     for (int k = threadIdx.x; k < kp.nmat; k += blockDim.x) s_mats[k] = kp.S.mats[k];
     for (int k = threadIdx.x; k < kp.S.nlights; k += blockDim.x) s_lights[k] = kp.S.lights[k];
@@ -314,218 +313,207 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     kp.S.lights = s_lights;
   }
 #endif
-  Counters cnt = {0, 0, 0, 0, 0, 0};
-  SplatCache sc;
-  unsigned nsamp = 0;
-  const float inv = 1.0f / (float)kp.sp.spp;
-  Paths<MAXV> P;
+}
+
+// Persistent waves: each wave takes work items (8x8 pixel block, chunk of spl samples) from a
+// global ticket counter until none are left, so per-item cost differences (path lengths, scene
+// regions) never leave CUs idle at the tail of the launch. Returns false at the first ticket past
+// the end (every wave reaches it). XCD mode: blocks b and b + 8 share an XCD (round-robin dealing,
+// MI355X_MICROARCH.md), so group g = b % 8 works through its own contiguous eighth of the items (a
+// contiguous band of pixel blocks, whose BVH region then stays in that XCD's L2) and only then
+// helps the other groups. Items are numbered from kp.item_lo.
+struct Item {
+  int x, y, s0, my_n;   // this lane's pixel and sample range [s0, s0 + my_n)
+  unsigned idx;         // item index relative to kp.item_lo
+};
+__device__ __forceinline__ bool next_item(const KParams& kp, int lane, int grp, int& cur, Item& it) {
+  unsigned item = 0;
+  if (kp.xcd) {
+    item = 0xffffffffu;
+    if (lane == 0) {
+      for (; cur < 8; cur++) {
+        const unsigned gg = (unsigned)((grp + cur) & 7);
+        const unsigned lo = gg * kp.region;
+        if (lo >= kp.nitems) continue;
+        const unsigned t = atomicAdd(kp.work8 + 32 * gg, 1u);
+        if (t < kp.region && lo + t < kp.nitems) { item = lo + t; break; }
+      }
+    }
+    item = __shfl(item, 0, 64);
+    cur = __shfl(cur, 0, 64);
+    if (item == 0xffffffffu) return false;
+  } else {
+    if (lane == 0) item = atomicAdd(kp.work, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= kp.nitems) return false;
+  }
+  it.idx = item;
+  item += kp.item_lo;
+  int chunk, blk;
+  if (kp.block_major) {
+    blk = (int)(item / kp.nchunks);
+    chunk = (int)(item - (unsigned)blk * kp.nchunks);
+  } else {
+    chunk = (int)(item / (unsigned)kp.nblocks);
+    blk = (int)(item - (unsigned)chunk * (unsigned)kp.nblocks);
+  }
+  int bx0, by0, bw, bh;
+  if (kp.blocks) {
+    int4 bb = kp.blocks[blk];
+    bx0 = bb.x; by0 = bb.y; bw = bb.z; bh = bb.w;
+  } else {
+    bx0 = (blk % kp.nbx) * 8;
+    by0 = (blk / kp.nbx) * 8;
+    bw = min(8, kp.sp.W - bx0);
+    bh = min(8, kp.sp.H - by0);
+  }
+  const int qx = lane & 7, qy = lane >> 3;
+  it.x = 0; it.y = 0;
+  int s0 = 0, s1 = 0;
+  if (qx < bw && qy < bh) {
+    it.x = bx0 + qx;
+    it.y = by0 + qy;
+    s0 = kp.spp_begin + chunk * kp.spl;
+    s1 = min(s0 + kp.spl, kp.spp_end);
+  }
+  it.s0 = s0;
+  it.my_n = max(0, s1 - s0);
+  return true;
+}
+
+// Per-wave connection state of one work item: the direct (s = 0) eye contributions and the
+// wave-uniform ring indices (the eye accumulators live in the ring's LDS).
+struct ConnState {
+  float dxs = 0, dys = 0, dzs = 0;
+  int head = 0, tail = 0;
 #ifdef BDPT_PHASE_PROF
-  unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
-#define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
-#else
-#define PH_STAMP(v)
+  unsigned long long ph_gen = 0, ph_flush = 0;
 #endif
-  // Persistent waves: each wave takes work items (8x8 pixel block, chunk of spl samples) from a
-  // global ticket counter until none are left, so per-item cost differences (path lengths, scene
-  // regions) never leave CUs idle at the tail of the launch. Every wave exits at the first
-  // ticket >= nitems.
-  // XCD mode: blocks b and b + 8 share an XCD (round-robin dealing, MI355X_MICROARCH.md), so group
-  // g = b % 8 works through its own contiguous eighth of the items (a contiguous band of pixel
-  // blocks, whose BVH region then stays in that XCD's L2) and only then helps the other groups.
-  const int grp = blockIdx.x & 7;
-  int cur = 0;   // wave-uniform: groups exhausted so far
-  for (;;) {
-    unsigned item = 0;
-    if (kp.xcd) {
-      item = 0xffffffffu;
-      if (lane == 0) {
-        for (; cur < 8; cur++) {
-          const unsigned gg = (unsigned)((grp + cur) & 7);
-          const unsigned lo = gg * kp.region;
-          if (lo >= kp.nitems) continue;
-          const unsigned t = atomicAdd(kp.work8 + 32 * gg, 1u);
-          if (t < kp.region && lo + t < kp.nitems) { item = lo + t; break; }
-        }
+};
+
+// The connections of one pixel-sample (est_radiance_global_illumination's s x t loop,
+// bidirection.cpp:472-500): the wave enumerates the (i, j) strategies in uniform nested loops,
+// so the j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
+// for all lanes instead of interleaving with the general case; every connection that needs a
+// visibility ray is pushed (ballot + mbcnt compaction) into the wave's LDS ring, and whenever 64
+// are queued the wave traces them together. PA: the path accessor (PathsInRegs over the lane's
+// private Paths).
+template <int LM, bool EXT, class PA>
+__device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, const PA& PP, Rng& g, int nE, int nL,
+                                               int lane, float inv, ConnState& cs, Counters& cnt) {
+  const int wE = wave_max(nE), wL = wave_max(nL);
+#ifdef BDPT_PHASE_PROF
+  const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+  unsigned long long tp0, tp1;
+#endif
+  // one (i, j) connection per lane (active lanes only), its ray pushed into the wave's ring, the
+  // ring flushed whenever 64 rays are queued
+  auto conn_step = [&](int i, int j, bool active, const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr) {
+    int kind = CONN_NONE;
+    Conn cn;
+    if (active) {
+      kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre);
+      if (kind == CONN_DIRECT) {
+        cs.dxs += cn.val.x * inv;
+        cs.dys += cn.val.y * inv;
+        cs.dzs += cn.val.z * inv;
       }
-      item = __shfl(item, 0, 64);
-      cur = __shfl(cur, 0, 64);
-      if (item == 0xffffffffu) break;
-    } else {
-      if (lane == 0) item = atomicAdd(kp.work, 1u);
-      item = __shfl(item, 0, 64);
-      if (item >= kp.nitems) break;
     }
-    int chunk, blk;
-    if (kp.block_major) {
-      blk = (int)(item / kp.nchunks);
-      chunk = (int)(item - (unsigned)blk * kp.nchunks);
-    } else {
-      chunk = (int)(item / (unsigned)kp.nblocks);
-      blk = (int)(item - (unsigned)chunk * (unsigned)kp.nblocks);
+    const bool push = kind == CONN_RAY;
+    const unsigned long long m = __ballot(push);
+    if (push) {
+      const int slot = (cs.tail + lanes_below(m)) & (QCAP - 1);
+      q.ox[slot] = cn.o.x; q.oy[slot] = cn.o.y; q.oz[slot] = cn.o.z;
+      q.dx[slot] = cn.d.x; q.dy[slot] = cn.d.y; q.dz[slot] = cn.d.z;
+      q.tmax[slot] = cn.tmax;
+      const bool eye_t = cn.splat < 0;
+      q.vx[slot] = eye_t ? cn.val.x * inv : cn.val.x;
+      q.vy[slot] = eye_t ? cn.val.y * inv : cn.val.y;
+      q.vz[slot] = eye_t ? cn.val.z * inv : cn.val.z;
+      q.tgt[slot] = eye_t ? ~lane : cn.splat;
     }
-    int bx0, by0, bw, bh;
-    if (kp.blocks) {
-      int4 bb = kp.blocks[blk];
-      bx0 = bb.x; by0 = bb.y; bw = bb.z; bh = bb.w;
-    } else {
-      bx0 = (blk % kp.nbx) * 8;
-      by0 = (blk / kp.nbx) * 8;
-      bw = min(8, kp.sp.W - bx0);
-      bh = min(8, kp.sp.H - by0);
-    }
-    const int qx = lane & 7, qy = lane >> 3;
-    int x = 0, y = 0, s0 = 0, s1 = 0;
-    if (qx < bw && qy < bh) {
-      x = bx0 + qx;
-      y = by0 + qy;
-      s0 = kp.spp_begin + chunk * kp.spl;
-      s1 = min(s0 + kp.spl, kp.spp_end);
-    }
-    const int my_n = max(0, s1 - s0);
-    const int wave_n = wave_max(my_n);
-    q.acc[0][lane] = 0;
-    q.acc[1][lane] = 0;
-    q.acc[2][lane] = 0;
-    float dxs = 0, dys = 0, dzs = 0;   // direct (s = 0) eye contributions
-    int head = 0, tail = 0;            // wave-uniform ring indices
-    for (int t = 0; t < wave_n; t++) {
-      Rng g;
-      int nE = 0, nL = 0;
+    cs.tail += __popcll(m);
+    if (cs.tail - cs.head >= 64) {
       PH_STAMP(tp0);
-      if (t < my_n) {
-        prepare_sample<MAXV, LM, EXT>(kp.S, kp.sp, P, cnt, g, x, y, (uint32_t)(s0 + t));
-        nE = P.nE;
-        nL = P.nL;
-        nsamp++;
-      }
-      // wave-uniform (i, j) loops: every lane is at the same strategy at the same time, so the
-      // j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
-      // for all lanes instead of interleaving with the general case.
-      const int wE = wave_max(nE), wL = wave_max(nL);
-      PH_STAMP(tp1);
-  #ifdef BDPT_PHASE_PROF
-      ph_prep += tp1 - tp0;
-      unsigned long long tg0 = tp1;
-  #endif
-      // one (i, j) connection per lane (active lanes only), its ray pushed into the wave's ring,
-      // the ring flushed whenever 64 rays are queued
-      auto conn_step = [&](int i, int j, bool active, const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr) {
-        int kind = CONN_NONE;
-        Conn cn;
-        if (active) {
-          kind = make_conn<EXT>(kp.S, kp.sp, PathsInRegs<MAXV>(P), g, i, j, cn, ev_pre, lv_pre);
-          if (kind == CONN_DIRECT) {
-            dxs += cn.val.x * inv;
-            dys += cn.val.y * inv;
-            dzs += cn.val.z * inv;
-          }
-        }
-        const bool push = kind == CONN_RAY;
-        const unsigned long long m = __ballot(push);
-        if (push) {
-          const int slot = (tail + lanes_below(m)) & (QCAP - 1);
-          q.ox[slot] = cn.o.x; q.oy[slot] = cn.o.y; q.oz[slot] = cn.o.z;
-          q.dx[slot] = cn.d.x; q.dy[slot] = cn.d.y; q.dz[slot] = cn.d.z;
-          q.tmax[slot] = cn.tmax;
-          const bool eye_t = cn.splat < 0;
-          q.vx[slot] = eye_t ? cn.val.x * inv : cn.val.x;
-          q.vy[slot] = eye_t ? cn.val.y * inv : cn.val.y;
-          q.vz[slot] = eye_t ? cn.val.z * inv : cn.val.z;
-          q.tgt[slot] = eye_t ? ~lane : cn.splat;
-        }
-        tail += __popcll(m);
-        if (tail - head >= 64) {
-          PH_STAMP(tp0);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-#if BDPT_FLUSH_REFILL
-          flush_refill<LM>(kp.S, q, head, tail, lane, kp.light, cnt, sc);
-          __builtin_amdgcn_wave_barrier();
-          head = tail;
-#else
-          flush_queue<LM>(kp.S, q, head, 64, lane, kp.light, cnt);
-          __builtin_amdgcn_wave_barrier();
-          head += 64;
-#endif
-          PH_STAMP(tp1);
-  #ifdef BDPT_PHASE_PROF
-          ph_flush += tp1 - tp0;
-  #endif
-        }
-      };
-#if BDPT_CONN_COMPACT
-      // The special strategies wave-uniformly: s = 0 (j = 0), the fresh light sample (j = 1),
-      // light tracing to the camera (i = 1, j >= 2) ...
-      for (int i = 2; i < wE; i++) conn_step(i, 0, i < nE);
-      for (int i = 1; i < wE; i++) conn_step(i, 1, i < nE && nL > 1);
-      for (int j = 2; j < wL; j++) conn_step(1, j, j < nL);
-      // ... then the general (i >= 2, j >= 2) pairs from per-lane lists of connectable vertices:
-      // a lane walks its own (i, j) pairs, so the wave iterates max(pairs) times instead of
-      // max|E| x max|L| (most cells of that grid are empty for most lanes)
-      unsigned mE = 0, mL = 0;
-      for (int k = 2; k < nE; k++) mE |= (P.E[k - 2].cq > 0.0f ? 1u : 0u) << k;
-      for (int k = 2; k < nL; k++) mL |= (P.L[k - 1].cq > 0.0f ? 1u : 0u) << k;
-      if (mL == 0) mE = 0;
-      unsigned jm = mL;
-      while (__ballot(mE != 0)) {
-        const bool act = mE != 0;
-        const int ci = act ? __builtin_ctz(mE) : 0, cj = act ? __builtin_ctz(jm) : 0;
-        conn_step(ci, cj, act);
-        if (act) {
-          jm &= jm - 1;
-          if (jm == 0) { mE &= mE - 1; jm = mL; }
-        }
-      }
-#elif BDPT_CONN_ORDER == 1
-      // E[i] loaded once per i and kept in registers across the j loop
-      for (int i = 1; i < wE; i++) {
-        const Vtx ev = P.E[i >= 2 ? i - 2 : 0];
-        for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL, i >= 2 ? &ev : nullptr);
-      }
-#elif BDPT_CONN_ORDER == 2
-      // j outer: L[j] loaded once per j and kept in registers across the i loop (the connections
-      // are order-free: per-connection RNG sub-streams, sums are fp32 atomics anyway)
-      for (int j = 0; j < wL; j++) {
-        const Vtx lv = P.L[j >= 1 ? j - 1 : 0];
-        for (int i = 1; i < wE; i++) conn_step(i, j, i < nE && j < nL, nullptr, j >= 1 ? &lv : nullptr);
-      }
-#else
-      for (int i = 1; i < wE; i++)
-      for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
-#endif
-  #ifdef BDPT_PHASE_PROF
-      ph_gen += __builtin_amdgcn_s_memtime() - tg0;
-  #endif
-    }
-    if (tail > head) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-#if BDPT_FLUSH_REFILL
-      flush_refill<LM>(kp.S, q, head, tail, lane, kp.light, cnt, sc);
-#else
-      flush_queue<LM>(kp.S, q, head, tail - head, lane, kp.light, cnt);
-#endif
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (my_n > 0) {
-      float ax = q.acc[0][lane] + dxs, ay = q.acc[1][lane] + dys, az = q.acc[2][lane] + dzs;
-      float* e = kp.eye + 3 * ((size_t)x + (size_t)y * kp.sp.W);
-      if (ax != 0) atomicAdd(e, ax);
-      if (ay != 0) atomicAdd(e + 1, ay);
-      if (az != 0) atomicAdd(e + 2, az);
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  sc.flush(kp.light, lane);
+      flush_queue<LM>(kp.S, q, cs.head, 64, lane, kp.light, cnt);
+      __builtin_amdgcn_wave_barrier();
+      cs.head += 64;
+      PH_STAMP(tp1);
 #ifdef BDPT_PHASE_PROF
-  if (lane == 0) {
-    atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
-    atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
-    atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
-    atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
-  }
+      cs.ph_flush += tp1 - tp0;
 #endif
+    }
+  };
+#if BDPT_CONN_COMPACT
+  // The special strategies wave-uniformly: s = 0 (j = 0), the fresh light sample (j = 1),
+  // light tracing to the camera (i = 1, j >= 2) ...
+  for (int i = 2; i < wE; i++) conn_step(i, 0, i < nE);
+  for (int i = 1; i < wE; i++) conn_step(i, 1, i < nE && nL > 1);
+  for (int j = 2; j < wL; j++) conn_step(1, j, j < nL);
+  // ... then the general (i >= 2, j >= 2) pairs from per-lane lists of connectable vertices:
+  // a lane walks its own (i, j) pairs, so the wave iterates max(pairs) times instead of
+  // max|E| x max|L| (most cells of that grid are empty for most lanes)
+  unsigned mE = 0, mL = 0;
+  for (int k = 2; k < nE; k++) mE |= (PP.e(k).cq > 0.0f ? 1u : 0u) << k;
+  for (int k = 2; k < nL; k++) mL |= (PP.l(k).cq > 0.0f ? 1u : 0u) << k;
+  if (mL == 0) mE = 0;
+  unsigned jm = mL;
+  while (__ballot(mE != 0)) {
+    const bool act = mE != 0;
+    const int ci = act ? __builtin_ctz(mE) : 0, cj = act ? __builtin_ctz(jm) : 0;
+    conn_step(ci, cj, act);
+    if (act) {
+      jm &= jm - 1;
+      if (jm == 0) { mE &= mE - 1; jm = mL; }
+    }
+  }
+#elif BDPT_CONN_ORDER == 1
+  // E[i] loaded once per i and kept in registers across the j loop
+  for (int i = 1; i < wE; i++) {
+    const Vtx ev = PP.e(i >= 2 ? i : 2);
+    for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL, i >= 2 ? &ev : nullptr);
+  }
+#elif BDPT_CONN_ORDER == 2
+  // j outer: L[j] loaded once per j and kept in registers across the i loop (the connections
+  // are order-free: per-connection RNG sub-streams, sums are fp32 atomics anyway)
+  for (int j = 0; j < wL; j++) {
+    const Vtx lv = PP.l(j >= 1 ? j : 1);
+    for (int i = 1; i < wE; i++) conn_step(i, j, i < nE && j < nL, nullptr, j >= 1 ? &lv : nullptr);
+  }
+#else
+  for (int i = 1; i < wE; i++)
+    for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
+#endif
+#ifdef BDPT_PHASE_PROF
+  cs.ph_gen += __builtin_amdgcn_s_memtime() - tg0;
+#endif
+}
+
+// End of a work item: the queued rays are traced and every lane adds its eye-image sum once.
+template <int LM>
+__device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const Item& it, int lane, ConnState& cs,
+                                            Counters& cnt) {
+  if (cs.tail > cs.head) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    flush_queue<LM>(kp.S, q, cs.head, cs.tail - cs.head, lane, kp.light, cnt);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (it.my_n > 0) {
+    float ax = q.acc[0][lane] + cs.dxs, ay = q.acc[1][lane] + cs.dys, az = q.acc[2][lane] + cs.dzs;
+    float* e = kp.eye + 3 * ((size_t)it.x + (size_t)it.y * kp.sp.W);
+    if (ax != 0) atomicAdd(e, ax);
+    if (ay != 0) atomicAdd(e + 1, ay);
+    if (az != 0) atomicAdd(e + 2, az);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const KParams& kp, int lane, unsigned nsamp, const Counters& cnt) {
   if (STATS) {
     unsigned v[8] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes};
 #pragma unroll
@@ -534,6 +522,74 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
     }
   }
+}
+
+// LM (LDS mode): 0 = scene read from HBM/L2; 1 = whole BVH + geometry staged in LDS by every
+// block; 2 = the top n_top BFS-ordered nodes (the part every ray traverses) staged in LDS.
+// EXT: environment light and/or Russian roulette (DESIGN.md §9); EXT = false is the reference-only
+// path with no trace of either in the generated code.
+template <int MAXV, bool STATS, int LM, bool EXT>
+__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
+  // One dynamic LDS array: [wave queues][optional scene / treelet copy]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#if BDPT_MATS_LDS
+  __shared__ DMat s_mats[kLdsMats];
+  __shared__ DLight s_lights[kLdsLights];
+#else
+  DMat* s_mats = nullptr;
+  DLight* s_lights = nullptr;
+#endif
+  stage_scene<LM>(kp, smem, s_mats, s_lights);
+  WaveQ* qs = (WaveQ*)smem;
+  const int lane = threadIdx.x & 63;
+  WaveQ& q = qs[threadIdx.x >> 6];
+  Counters cnt = {0, 0, 0, 0, 0, 0};
+  unsigned nsamp = 0;
+  const float inv = 1.0f / (float)kp.sp.spp;
+  Paths<MAXV> P;
+#ifdef BDPT_PHASE_PROF
+  unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
+#endif
+  const int grp = blockIdx.x & 7;
+  int cur = 0;   // wave-uniform: XCD groups exhausted so far
+  Item it;
+  while (next_item(kp, lane, grp, cur, it)) {
+    const int wave_n = wave_max(it.my_n);
+    q.acc[0][lane] = 0;
+    q.acc[1][lane] = 0;
+    q.acc[2][lane] = 0;
+    ConnState cs;
+    for (int t = 0; t < wave_n; t++) {
+      Rng g;
+      int nE = 0, nL = 0;
+      PH_STAMP(tp0);
+      if (t < it.my_n) {
+        prepare_sample<MAXV, LM, EXT>(kp.S, kp.sp, P, cnt, g, it.x, it.y, (uint32_t)(it.s0 + t));
+        nE = P.nE;
+        nL = P.nL;
+        nsamp++;
+      }
+      PH_STAMP(tp1);
+#ifdef BDPT_PHASE_PROF
+      ph_prep += tp1 - tp0;
+#endif
+      connect_sample<LM, EXT>(kp, q, PathsInRegs<MAXV>(P), g, nE, nL, lane, inv, cs, cnt);
+    }
+    finish_item<LM>(kp, q, it, lane, cs, cnt);
+#ifdef BDPT_PHASE_PROF
+    ph_gen += cs.ph_gen;
+    ph_flush += cs.ph_flush;
+#endif
+  }
+#ifdef BDPT_PHASE_PROF
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
+    atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
+    atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
+    atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
+  }
+#endif
+  flush_stats<STATS>(kp, lane, nsamp, cnt);
 }
 
 // k_pt: the unidirectional PathTracer (bdpt_core.h pt_pixel). Persistent waves take 8x8 pixel
@@ -661,8 +717,8 @@ int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
   return BDPT_OK;
 }
 
-template <int MAXV, bool STATS, bool EXT>
-int launch_lm(Ctx* c, KParams& kp) {
+// The LDS mode of a BDPT launch and the dynamic LDS it needs (wave queues + the scene copy).
+int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
   const size_t q = kWavesPerBlock * sizeof(WaveQ);
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const bool has_nodes = !c->hs.bvh2.nodes.empty();
@@ -679,10 +735,18 @@ int launch_lm(Ctx* c, KParams& kp) {
   if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
   if (lm == 2 && c->env_ntop_max >= 0) kp.S.ntop = std::min(kp.S.ntop, c->env_ntop_max);   // diagnostics
   c->last_lm = lm;
-  if (lm == 3) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 3, EXT>, q + flat, kp);
-  if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, q + full, kp);
-  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, q + (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp);
-  return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0, EXT>, q, kp);
+  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
+  return lm;
+}
+
+template <int MAXV, bool STATS, bool EXT>
+int launch_lm(Ctx* c, KParams& kp) {
+  size_t lds = 0;
+  const int lm = pick_lm(c, kp, &lds);
+  if (lm == 3) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 3, EXT>, lds, kp);
+  if (lm == 1) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 1, EXT>, lds, kp);
+  if (lm == 2) return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 2, EXT>, lds, kp);
+  return launch_persistent(c, k_bdpt_sample<MAXV, STATS, 0, EXT>, lds, kp);
 }
 
 template <int MAXV>
@@ -893,6 +957,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.prof = c->d_stats + 8;
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   kp.nmat = (int)c->hs.mats.size();
+  kp.item_lo = 0;
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);
