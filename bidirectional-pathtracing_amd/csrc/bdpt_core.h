@@ -1148,6 +1148,8 @@ struct Paths {
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
   uint32_t dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
   float l1_dir_pdf;
+  f3 l1_d;           // the light walk's first direction and its pdf (read back when it starts)
+  float l1_pdf;
 };
 
 struct SampleParams {
@@ -1480,6 +1482,16 @@ struct PathsInRegs {
 // eye walk ends starts its light walk in the next iteration, so a wave iterates
 // max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
 // sample + walk: 1) make the interleaving invisible in the results.
+// Drop the RNG's cached Philox block before each walk traversal: 4 fewer registers live across it,
+// at most one extra Philox evaluation per bounce. Measured slower (fewer spills, more VALU): off.
+#ifndef BDPT_RNG_DROP
+#define BDPT_RNG_DROP 0   // measured: off is +1% (Lucy stand-in 591 -> 598, CBspheres +1.3%)
+#endif
+// 0: light sample drawn before the walk and held in registers; 1: drawn when the eye walk ends;
+// 2: drawn before the walk, read back from the path store when the light walk starts
+#ifndef BDPT_LATE_LIGHT
+#define BDPT_LATE_LIGHT 2
+#endif
 template <int MAXV, int LM = 0, bool EXT = false>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
@@ -1491,20 +1503,19 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   float dx = px / (float)sp.W, dy = py / (float)sp.H;
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   f3 rd = camera_dir(S.cam, dx, dy);
-  // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le, on stream 1
-  f3 lo, ld, ln;
-  float lpp, ldp;
-  float mis_p, mis_dir;   // L[1]'s MIS densities (differ from lpp / ldp only for the env light)
-  f3 lrad;
-  uint32_t lpos;
+  // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le, on stream 1: the
+  // light vertex L[1] and the light walk's first ray. BDPT_LATE_LIGHT: drawn when the lane's eye
+  // walk ends instead of before it (same stream, same values), so the ~17 registers of the light
+  // sample are not live across the eye walk's traversals.
   bool l1env = false;
-  {
-    Rng gl = g;
+  float mis_p = 0.0f;   // L[1]'s MIS point density (differs from lpp only for the env light)
+  auto sample_light = [&](Rng& gl, f3& lo, f3& ld, f3& ln, f3& alpha1, float& ldp) {
     rng_stream(gl, 1);
     int lid = (int)(rng_next(gl) * (float)S.nlights);
     if (lid >= S.nlights) lid = S.nlights - 1;
     const DLight& L0 = S.lights[lid];
-    lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
+    f3 lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
+    float lpp, mis_dir;
     if (EXT && L0.type == LIGHT_ENV) {
       // sample_Le of the environment light: direction by sample_L's importance
       // sampling, origin uniform on the disk of radius R facing -w, tangent to the bounding sphere
@@ -1555,27 +1566,39 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       mis_p = lpp;
       mis_dir = ldp;
     }
-    lpos = gl.pos;
-  }
-  lpp = lpp / (float)S.nlights;
-  mis_p = mis_p / (float)S.nlights;
-  {
+    lpp = lpp / (float)S.nlights;
+    mis_p = mis_p / (float)S.nlights;
+    alpha1 = divs(lrad, lpp);
     Vtx& v1 = P.L[0];
     v1.pos = lo;
     v1.n = ln;
     v1.zh = l1env ? ln : zaxis(ln);
-    v1.alpha = divs(lrad, lpp);
+    v1.alpha = alpha1;
     v1.mat = l1env ? (int)MAT_ENV_V : -1;
     v1.gp = 0; v1.cq = 0;
     v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused walk)
-  }
-  P.l1_dir_pdf = mis_dir;
+    P.l1_dir_pdf = mis_dir;
+  };
+#if BDPT_LATE_LIGHT != 1
+  Rng gl0 = g;
+  f3 lo, ld, ln, la1;
+  float ldp;
+  sample_light(gl0, lo, ld, ln, la1, ldp);
+  const uint32_t lpos = gl0.pos;
+#if BDPT_LATE_LIGHT == 2
+  P.l1_d = ld;
+  P.l1_pdf = ldp;
+  l1env = false;   // re-read with the rest when the light walk starts
+#endif
+#endif
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
   f3 ro = cam;
   float rmin = S.cam.nclip, rmax = S.cam.fclip;
-  f3 prev_alpha = divs(splat3(1.0f), 1.0f);
-  float prev_pdf = 1.0f;
-  f3 prev_f = splat3(1.0f), prev_n = rd;
+  f3 prev_n = rd;
+  // the next vertex's throughput alpha = prev_alpha * |cos| * f / pdf (prepare_bidirectional_subpath
+  // :60-62), formed when its ray is: one f3 live across the traversal instead of alpha, f and pdf
+  auto next_alpha = [](f3 pa, f3 pn, f3 d, f3 f, float pdf) { return divs(mul(muls(pa, fabsf(dot(pn, d))), f), pdf); };
+  f3 nalpha = next_alpha(divs(splat3(1.0f), 1.0f), prev_n, rd, splat3(1.0f), 1.0f);
   int i = 2, count = 0;
   uint32_t dm = 0;
   bool light = false;
@@ -1589,6 +1612,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
 #endif
+#if BDPT_RNG_DROP
+    g.cur = 0xffffffffu;   // the Philox block cache is not kept across the traversal (recomputed)
+#endif
     bool end = !trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     cnt.clk_walk_trace += __builtin_amdgcn_s_memtime() - tq0;
@@ -1596,7 +1622,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     if (EXT && end && !light && S.env.light >= 0) {
       // an escaped eye ray ends on the environment light: vertex at infinity in direction rd
       Vtx v;
-      v.alpha = divs(mul(muls(prev_alpha, fabsf(dot(prev_n, rd))), prev_f), prev_pdf);
+      v.alpha = nalpha;
       v.pos = ro;
       v.n = neg(rd);
       v.zh = v.n;
@@ -1618,7 +1644,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       const Frame fr = make_frame(n);
       const f3 hit_p = add(ro, muls(rd, h.t));
       Vtx v;
-      v.alpha = divs(mul(muls(prev_alpha, fabsf(dot(prev_n, rd))), prev_f), prev_pdf);
+      v.alpha = nalpha;
       v.pos = hit_p;
       v.n = n;
       v.zh = fr.Z;
@@ -1688,10 +1714,8 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         rd = normalize(to_world(fr, wi));
         rmin = BDPT_EPS_F;
         rmax = INFINITY;
-        prev_f = fv;
         prev_n = n;
-        prev_pdf = pdf * q;
-        prev_alpha = v.alpha;
+        nalpha = next_alpha(v.alpha, n, rd, fv, pdf * q);
         i++;
       }
     }
@@ -1704,13 +1728,29 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       P.nE = count + 2;
       P.dE = dm;
       light = true;
+#if BDPT_LATE_LIGHT == 1
+      {
+        f3 a1;
+        float pdf1;
+        sample_light(g, ro, rd, prev_n, a1, pdf1);
+        nalpha = next_alpha(a1, prev_n, rd, splat3(1.0f), pdf1);
+      }
+#elif BDPT_LATE_LIGHT == 2
+      // the light sample drawn before the eye walk, read back from the path store (not held in
+      // registers across the eye walk)
       rng_stream(g, 1);
       g.pos = lpos;
-      ro = lo; rd = ld; rmin = BDPT_EPS_F; rmax = INFINITY;
-      prev_alpha = divs(lrad, lpp);
-      prev_pdf = ldp;
-      prev_f = splat3(1.0f);
-      prev_n = ln;
+      ro = P.L[0].pos; rd = P.l1_d; prev_n = P.L[0].n;
+      nalpha = next_alpha(P.L[0].alpha, prev_n, rd, splat3(1.0f), P.l1_pdf);
+      mis_p = P.L[0].fwd;
+      l1env = P.L[0].mat == (int)MAT_ENV_V;
+#else
+      rng_stream(g, 1);
+      g.pos = lpos;
+      ro = lo; rd = ld; prev_n = ln;
+      nalpha = next_alpha(la1, prev_n, rd, splat3(1.0f), ldp);
+#endif
+      rmin = BDPT_EPS_F; rmax = INFINITY;
       i = 2; count = 0; dm = 0;
 #if BDPT_FUSED_CONSTANTS
       pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
@@ -1719,7 +1759,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   }
   if (!BDPT_FUSED_CONSTANTS) {
     eye_constants<MAXV, EXT>(S, P);
-    light_constants<MAXV, EXT>(S, P, mis_p);
+    light_constants<MAXV, EXT>(S, P, P.L[0].fwd);
   }
 }
 

@@ -382,7 +382,11 @@ __device__ __forceinline__ bool next_item(const KParams& kp, int lane, int grp, 
 }
 
 // Per-wave connection state of one work item: the direct (s = 0) eye contributions and the
-// wave-uniform ring indices (the eye accumulators live in the ring's LDS).
+// wave-uniform ring indices (the eye accumulators live in the ring's LDS). BDPT_DIRECT_LDS: the
+// direct contributions go to the LDS accumulators too.
+#ifndef BDPT_DIRECT_LDS
+#define BDPT_DIRECT_LDS 1
+#endif
 struct ConnState {
   float dxs = 0, dys = 0, dzs = 0;
   int head = 0, tail = 0;
@@ -414,9 +418,17 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
     if (active) {
       kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre);
       if (kind == CONN_DIRECT) {
+#if BDPT_DIRECT_LDS
+        // straight into this lane's accumulator in the wave's LDS (only this wave writes it, and
+        // not while a flush runs): no registers held across the walks
+        q.acc[0][lane] += cn.val.x * inv;
+        q.acc[1][lane] += cn.val.y * inv;
+        q.acc[2][lane] += cn.val.z * inv;
+#else
         cs.dxs += cn.val.x * inv;
         cs.dys += cn.val.y * inv;
         cs.dzs += cn.val.z * inv;
+#endif
       }
     }
     const bool push = kind == CONN_RAY;
