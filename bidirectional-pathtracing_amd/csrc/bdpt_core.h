@@ -224,6 +224,9 @@ struct EnvView {
   const float* cond;   // w*h: conds_y (per-row CDFs)
   const float* pdf;    // w*h: pdf_envmap
   const float* rgb;    // w*h*3: data[w*j + i]
+  const int* gmarg;    // gm+1: guide table of marg (null: plain binary search)
+  const int* gcond;    // h*(gc+1): guide tables of the rows of cond
+  int gm, gc;
   int w, h;
   int light;           // index of the env light in the light list (-1: none)
   float cx, cy, cz, rad;
@@ -375,6 +378,10 @@ namespace bdpt {
 #endif
 static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
               "BVH widths must be 2 or 4");
+// Any-hit (connection-ray) traversal order: 0 = children in slot order, 1 = near-first like closest hit
+#ifndef BDPT_ANY_ORD
+#define BDPT_ANY_ORD 0
+#endif
 // LM 3: walk the flat list as one run of primitives with the next record prefetched (S.fn > 0)
 #ifndef BDPT_FLAT_PREFETCH
 #define BDPT_FLAT_PREFETCH 1
@@ -749,7 +756,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       if (li >= S.nleaves) return false;
       ref = ld_lds_i(S.lleaves + li++);
     }
-    while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
+    while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
     float4 a0, a1, a2;
@@ -821,7 +828,7 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
 template <int LM, int K>
 BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
                                          int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, false>(S, r, ref, tmin, tmax, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
   if (ref == kTravDone) { *hit = false; return true; }
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -1051,6 +1058,20 @@ BDPT_HD int upper_idx(const float* a, int n, float u) {   // std::upper_bound(a,
   }
   return lo < n ? lo : n - 1;
 }
+// The same index through a guide table gd[0..G] (gd[k] = upper_bound(a, a + n, k / G), G a power of
+// two, bdpt_scene.cpp): u * G is exact, so the answer lies in [gd[k], gd[k + 1]] for k = floor(u * G)
+// and only that range is searched (one or two dependent loads instead of log2 n).
+BDPT_HD int upper_idx_guided(const float* a, int n, const int* gd, int G, float u) {
+  int k = (int)(u * (float)G);
+  k = k < 0 ? 0 : k > G - 1 ? G - 1 : k;
+  int lo = gd[k], cnt = gd[k + 1] - lo;
+  while (cnt > 0) {
+    const int st = cnt >> 1, m = lo + st;
+    if (!(u < a[m])) { lo = m + 1; cnt -= st + 1; }
+    else cnt = st;
+  }
+  return lo < n ? lo : n - 1;
+}
 BDPT_HD f3 env_texel(const EnvView& E, int k) {
   const float* p = E.rgb + 3 * (size_t)k;
   return mk3(p[0], p[1], p[2]);
@@ -1110,8 +1131,14 @@ BDPT_HD float env_pdf_dir(const EnvView& E, f3 u) {
 BDPT_HD f3 env_sample_dir(const EnvView& E, Rng& g, f3* w, float* pdf) {
   float ux, uy;
   grid2d(g, &ux, &uy);
-  const int y = upper_idx(E.marg, E.h, uy);
-  const int x = upper_idx(E.cond + (size_t)E.w * y, E.w, ux);
+  int y, x;
+  if (E.gmarg) {
+    y = upper_idx_guided(E.marg, E.h, E.gmarg, E.gm, uy);
+    x = upper_idx_guided(E.cond + (size_t)E.w * y, E.w, E.gcond + (size_t)(E.gc + 1) * y, E.gc, ux);
+  } else {
+    y = upper_idx(E.marg, E.h, uy);
+    x = upper_idx(E.cond + (size_t)E.w * y, E.w, ux);
+  }
   const float xf = (float)x + rng_next(g);
   const float yf = (float)y + rng_next(g);
   float st;

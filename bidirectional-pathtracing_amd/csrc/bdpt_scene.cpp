@@ -353,12 +353,30 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
     }
     out.env_w = w;
     out.env_h = h;
-    out.env.resize((size_t)h + np * 2 + np * 3);
+    // guide tables (cut-point method) for the device's CDF inversions: cell k of a CDF a[0..n) holds
+    // upper_bound(a, a + n, k / G), so upper_bound(u) lies in [guide[k], guide[k + 1]] for
+    // k = floor(u * G) (exact for a power-of-two G) and a short search finds the reference's index
+    int gm = 1, gc = 1;
+    while (gm < h) gm <<= 1;
+    while (gc < w) gc <<= 1;
+    out.env_gm = gm;
+    out.env_gc = gc;
+    out.env.resize((size_t)h + np * 2 + np * 3 + (size_t)(gm + 1) + (size_t)h * (gc + 1));
     float* o = out.env.data();
+    const float* fmarg = o;
     for (int j = 0; j < h; j++) *o++ = (float)marg[j];
+    const float* fcond = o;
     for (size_t k = 0; k < np; k++) *o++ = (float)cond[k];
     for (size_t k = 0; k < np; k++) *o++ = (float)pdf[k];
     for (size_t k = 0; k < np * 3; k++) *o++ = em.rgb[k];
+    auto guide = [&o](const float* a, int n, int g) {
+      for (int k = 0; k <= g; k++) {
+        const int32_t v = (int32_t)(std::upper_bound(a, a + n, (float)k / (float)g) - a);
+        std::memcpy(o++, &v, sizeof v);
+      }
+    };
+    guide(fmarg, h, gm);
+    for (int j = 0; j < h; j++) guide(fcond + (size_t)w * j, w, gc);
     // bounding sphere of the primitives (the emission disk's radius and centre)
     double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < n; i++)

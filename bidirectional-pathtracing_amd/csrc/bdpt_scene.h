@@ -49,7 +49,9 @@ struct HostScene {
   // (environment_light.cpp:18-62) built in fp64 and rounded, and the emission sphere
   int env_light = -1;         // index in `lights`, -1 = none
   int env_w = 0, env_h = 0;
-  std::vector<float> env;     // marginal_y[h] | conds_y[w*h] | pdf_envmap[w*h] | rgb[w*h*3]
+  std::vector<float> env;     // marginal_y[h] | conds_y[w*h] | pdf_envmap[w*h] | rgb[w*h*3] |
+                              // guide tables (int32 bits): marginal[gm+1] | per row conditional[h*(gc+1)]
+  int env_gm = 0, env_gc = 0; // guide-table cells (powers of two)
   float env_c[3] = {0, 0, 0}, env_rad = 0;
 };
 

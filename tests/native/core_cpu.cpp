@@ -47,6 +47,10 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.env.cond = hs.env.data() + hs.env_h;
   S.env.pdf = hs.env.data() + hs.env_h + np;
   S.env.rgb = hs.env.data() + hs.env_h + 2 * np;
+  S.env.gmarg = hs.env.empty() ? nullptr : (const int*)(hs.env.data() + hs.env_h + 5 * np);
+  S.env.gcond = hs.env.empty() ? nullptr : S.env.gmarg + hs.env_gm + 1;
+  S.env.gm = hs.env_gm;
+  S.env.gc = hs.env_gc;
   S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];
   S.env.rad = hs.env_rad;
   SampleParams sp;
@@ -161,6 +165,10 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
   S.env.cond = hs.env.data() + hs.env_h;
   S.env.pdf = hs.env.data() + hs.env_h + np;
   S.env.rgb = hs.env.data() + hs.env_h + 2 * np;
+  S.env.gmarg = hs.env.empty() ? nullptr : (const int*)(hs.env.data() + hs.env_h + 5 * np);
+  S.env.gcond = hs.env.empty() ? nullptr : S.env.gmarg + hs.env_gm + 1;
+  S.env.gm = hs.env_gm;
+  S.env.gc = hs.env_gc;
   S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];
   S.env.rad = hs.env_rad;
   PtParams pp;

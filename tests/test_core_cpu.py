@@ -67,7 +67,9 @@ def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M, lds_mode)
 
 EXT_CASES = [("CBspheres_lambertian", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 5, False, True),
              ("CBempty", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 8, True, False),
-             ("CBgems", 32, 24, 1, 7, True, True), ("CBspheres_lambertian", 24, 18, 2, 8, True, True)]
+             ("CBgems", 32, 24, 1, 7, True, True), ("CBspheres_lambertian", 24, 18, 2, 8, True, True),
+             # non-power-of-two map: the guide tables' cells (powers of two) straddle CDF entries
+             ("CBspheres_lambertian", 24, 18, 4, 5, False, (37, 19))]
 
 
 @pytest.mark.parametrize("lds_mode", [0, 1])
@@ -79,7 +81,7 @@ def test_device_pipeline_bit_exact_env_rr(name, W, H, spp, M, rr, env, lds_mode)
     from envmap import synth_envmap
     sc = golden_scene(name, W, H)
     if env:
-        sc.set_envmap(synth_envmap(32, 16))
+        sc.set_envmap(synth_envmap(*(env if isinstance(env, tuple) else (32, 16))))
     eye, light, st = core_render(sc, W, H, spp, M, seed=99, lds_mode=lds_mode, rr=rr)
     _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=99, threads=1, rr=rr)
     assert np.isfinite(eye).all() and np.isfinite(light).all()

@@ -19,8 +19,14 @@ launches = int(sys.argv[6]) if len(sys.argv) > 6 else 2
 if os.environ.get("BDPT_LIB"):   # a variant build replaces the default library (loaded once)
     B._lib = B.load_library(os.environ["BDPT_LIB"])
 sc = B.load_dae(scene, W, H) if scene.endswith(".dae") else golden_scene(scene, W, H)
+if os.environ.get("BDPT_ENV"):   # synth:WxH: the synthetic sky of tools/envmap.py (C5's stand-in map)
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from envmap import synth_envmap
+    ew, eh = (int(v) for v in os.environ["BDPT_ENV"].split(":")[1].split("x"))
+    sc.set_envmap(synth_envmap(ew, eh))
 pt = B.BidirectionalPathTracer(sc, W, H, spp * launches, M, seed=5489, samples_per_lane=int(os.environ.get("BDPT_SPL", "0")),
-                               collect_stats=os.environ.get("BDPT_STATS") == "1")
+                               collect_stats=os.environ.get("BDPT_STATS") == "1",
+                               russian_roulette=os.environ.get("BDPT_RR") == "1")
 if os.environ.get("BDPT_WARM", "1") == "1":   # code-object load + first-launch setup, untimed
     pt.raytrace_tiles([], 0, 1)
     pt.sync()
