@@ -49,6 +49,10 @@ WORKLOADS = {
 }
 HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_NODE, BYTES_TRI, BYTES_SPH, BYTES_HIT = 32, 36, 16, 40
+# environment-light table reads (bdpt_stats v6): a sampled direction reads 2 guide
+# cells + 2 CDF entries per axis (marginal, row), the texel pdf and 4 texels; a radiance lookup 4
+# texels; a pdf lookup one texel pdf
+BYTES_ENV_SAMPLE, BYTES_ENV_LOOKUP, BYTES_ENV_PDF = 76, 48, 4
 
 
 def rank_sample_range(step: int, rank: int, world: int, spp: int, scaling: str = "strong"):
@@ -64,7 +68,12 @@ def rank_sample_range(step: int, rank: int, world: int, spp: int, scaling: str =
 
 def algorithmic_bytes(st) -> int:
     return (BYTES_NODE * st.node_visits + BYTES_TRI * st.tri_tests + BYTES_SPH * st.sph_tests
-            + BYTES_HIT * st.hits)
+            + BYTES_HIT * st.hits + env_bytes(st))
+
+
+def env_bytes(st) -> int:
+    return (BYTES_ENV_SAMPLE * st.env_samples + BYTES_ENV_LOOKUP * st.env_lookups
+            + BYTES_ENV_PDF * st.env_pdf_lookups)
 
 
 def global_memory_bytes(st) -> int:
@@ -75,7 +84,7 @@ def global_memory_bytes(st) -> int:
     nodes = st.node_visits - st.lds_node_visits
     prims = 0 if lm in (1, 3) else BYTES_TRI * st.tri_tests + BYTES_SPH * st.sph_tests
     hits = 0 if lm == 3 else BYTES_HIT * st.hits
-    return BYTES_NODE * nodes + prims + hits
+    return BYTES_NODE * nodes + prims + hits + env_bytes(st)
 
 
 def ensure_standin(path: str) -> None:
@@ -370,9 +379,10 @@ def main() -> int:
                      "kernel_ms": round(kern_ms, 3),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "note": "achieved = SURVEY §8d algorithmic scene bytes (32 B/child AABB, 36 B/triangle "
-                             "test, 16 B/sphere test, 40 B/closest hit) / launch time (HIP events on the ctx "
-                             "stream); gmem_* leaves out the scene reads served from the CU's LDS copy; "
-                             "traffic = measured HBM-side bytes (PMC)",
+                             "test, 16 B/sphere test, 40 B/closest hit; environment light: 76 B/sampled "
+                             "direction, 48 B/radiance lookup, 4 B/pdf lookup) / launch time (HIP events on "
+                             "the ctx stream); gmem_* leaves out the scene reads served from the CU's LDS "
+                             "copy; traffic = measured HBM-side bytes (PMC)",
                      "gmem_bytes_per_launch": gmem_launch,
                      "gmem_achieved": round(gmem_launch / (kern_ms * 1e-3) / 1e9, 2),
                      "gmem_frac": round(gmem_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
@@ -382,7 +392,9 @@ def main() -> int:
                                            "tri_tests": st.tri_tests,
                                            "sph_tests": st.sph_tests, "hits": st.hits,
                                            "closest_rays": st.closest_rays,
-                                           "shadow_rays": st.shadow_rays}},
+                                           "shadow_rays": st.shadow_rays,
+                                           "env_samples": st.env_samples, "env_lookups": st.env_lookups,
+                                           "env_pdf_lookups": st.env_pdf_lookups}},
     }
     if traffic_info:
         out["roofline"]["traffic_pmc"] = traffic_info

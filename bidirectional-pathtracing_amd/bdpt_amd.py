@@ -92,7 +92,8 @@ class Stats(C.Structure):
                 ("tri_tests", C.c_uint64), ("sph_tests", C.c_uint64), ("hits", C.c_uint64),
                 ("last_kernel_ms", C.c_double), ("bvh_nodes", C.c_uint64),
                 ("bvh_depth", C.c_uint64), ("lds_node_visits", C.c_uint64),
-                ("lds_mode", C.c_int32), ("reserved0", C.c_int32)]
+                ("lds_mode", C.c_int32), ("reserved0", C.c_int32),
+                ("env_samples", C.c_uint64), ("env_lookups", C.c_uint64), ("env_pdf_lookups", C.c_uint64)]
 
 
 class Scene:

@@ -270,6 +270,7 @@ struct SceneView {
 struct Counters {
   uint32_t nodes, tris, sphs, closest, shadow, hits;
   uint32_t lnodes = 0;   // of `nodes`: child AABBs read from the block's LDS copy (LM 1, LM 2 treelet)
+  uint32_t env_s = 0, env_l = 0, env_p = 0;   // environment-light samples / radiance / pdf lookups
 #ifdef BDPT_PHASE_PROF
   unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
 #endif
@@ -393,6 +394,13 @@ static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDT
 #define BDPT_LEAF_PREFETCH 1
 #endif
 BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM == 0 || LM == 2); }
+// With leaf_prefetch: the first record of a leaf is loaded where the descent produces the leaf
+// reference (inside the node loop, or at a pop), not after the wave's node loop ends, so the lanes
+// that reach their leaf early have the fetch in flight while the others still descend.
+#ifndef BDPT_LEAF_EARLY
+#define BDPT_LEAF_EARLY 1
+#endif
+BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY; }
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
@@ -666,16 +674,24 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     return h.prim >= 0;
   }
 #endif
+  float4 a0, a1, a2;
+  auto fetch_leaf = [&](int lr) {   // leaf_early: first record of leaf lr
+    const int s3 = 3 * leaf_start(lr);
+    a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
+  };
+  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
   for (;;) {
     if (LM == 3) {
       if (li >= S.nleaves) break;
       ref = ld_lds_i(S.lleaves + li++);
     }
-    while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
+    while (ref >= 0) {
+      ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
+      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+    }
     if (ref == kTravDone) break;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-    float4 a0, a1, a2;
-    if constexpr (leaf_prefetch(LM)) {
+    if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
@@ -716,6 +732,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       }
     }
     if (LM != 3 && !stk.pop(ref)) break;
+    if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
   }
   if (h.prim >= 0) c.hits++;
   return h.prim >= 0;
@@ -751,16 +768,24 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     return false;
   }
 #endif
+  float4 a0, a1, a2;
+  auto fetch_leaf = [&](int lr) {   // leaf_early: first record of leaf lr
+    const int s3 = 3 * leaf_start(lr);
+    a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
+  };
+  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
   for (;;) {
     if (LM == 3) {
       if (li >= S.nleaves) return false;
       ref = ld_lds_i(S.lleaves + li++);
     }
-    while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
+    while (ref >= 0) {
+      ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
+      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+    }
     if (ref == kTravDone) return false;
     const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-    float4 a0, a1, a2;
-    if constexpr (leaf_prefetch(LM)) {
+    if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
@@ -790,6 +815,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       if (ok) return true;
     }
     if (LM != 3 && !stk.pop(ref)) return false;
+    if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
   }
 }
 
@@ -1549,6 +1575,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       f3 w;
       float pw;
       lrad = env_sample_dir(S.env, gl, &w, &pw);
+      cnt.env_s++;
       const float u1 = rng_next(gl), u2 = rng_next(gl);
       const float r = S.env.rad * sqrtf(u1);
       float c, sn;
@@ -1806,9 +1833,10 @@ struct Conn {
 BDPT_HD bool can_connect(const Vtx& v) { return v.cq > 0.0f; }
 // ev_pre / lv_pre: E[i] / L[j] already loaded by the caller (kept across the megakernel's inner
 // connection loop), or null.
+// ec: environment-table read counters (stats builds), or null.
 template <bool EXT = false, class PA>
 BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, Rng& g, int i, int j, Conn& cn,
-                      const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr) {
+                      const Vtx* ev_pre = nullptr, const Vtx* lv_pre = nullptr, Counters* ec = nullptr) {
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   const bool eye_cam = i == 1;
   Vtx ev, lv;
@@ -1822,9 +1850,13 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
     if (eye_cam) return CONN_NONE;
     if (EXT && is_env(ev)) {   // an escaped eye ray: the environment light contains it (§9)
       const f3 c = env_radiance(S.env, neg(ev.n));
+      if (ec) ec->env_l++;
       f3 contrib = mul(mul(ev.alpha, splat3(1.0f)), c);
       float w = 0;
-      if (norm(contrib) > BDPT_EPS_F) w = mis_weight<EXT>(S, P, &ev, &lv, i, 0, ls, es, S.env.light, splat3(0), 0);
+      if (norm(contrib) > BDPT_EPS_F) {
+        w = mis_weight<EXT>(S, P, &ev, &lv, i, 0, ls, es, S.env.light, splat3(0), 0);
+        if (ec) ec->env_p++;   // the j = 0 weight's env_pdf_dir
+      }
       cn.val = muls(contrib, w);
       return CONN_DIRECT;
     }
@@ -1860,6 +1892,7 @@ BDPT_HD int make_conn(const SceneView& S, const SampleParams& sp, const PA& P, R
     if (EXT && S.lights[id].type == LIGHT_ENV) {
       if (eye_cam) return CONN_NONE;   // no camera connection to a vertex at infinity (§9)
       ls = env_sample_point(S, g, epos);
+      if (ec) ec->env_s++;
     } else {
       float lp;
       ls = light_sample_point(S.lights[id], S.nlights, g, epos, &lp);

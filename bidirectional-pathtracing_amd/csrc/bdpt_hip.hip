@@ -254,10 +254,14 @@ __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int h
 constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
 
 // Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
-// wave-uniform max|E| x max|L| grid (the special strategies stay wave-uniform).
+// wave-uniform max|E| x max|L| grid (the special strategies stay wave-uniform). 0 = never, 1 =
+// always, 2 = for the long-path kernels (MAXV >= 8, m > 5), where the grid is mostly empty: measured
+// C5-shaped (m8, env, RR) 446 -> 470, CBgems m7 +0.9%; the m5 north star -1.7% (so grid there).
 #ifndef BDPT_CONN_COMPACT
-#define BDPT_CONN_COMPACT 0
+#define BDPT_CONN_COMPACT 2
 #endif
+template <int MAXV>
+constexpr bool conn_compact() { return BDPT_CONN_COMPACT == 1 || (BDPT_CONN_COMPACT == 2 && MAXV >= 8); }
 // Connection loop order: 0 = the reference's (i outer, j inner), vertices reloaded per pair;
 // 1 = i outer with E[i] held across j; 2 = j outer with L[j] held across i.
 #ifndef BDPT_CONN_ORDER
@@ -402,7 +406,7 @@ struct ConnState {
 // visibility ray is pushed (ballot + mbcnt compaction) into the wave's LDS ring, and whenever 64
 // are queued the wave traces them together. PA: the path accessor (PathsInRegs over the lane's
 // private Paths).
-template <int LM, bool EXT, class PA>
+template <int LM, bool EXT, bool COMPACT, bool STATS, class PA>
 __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, const PA& PP, Rng& g, int nE, int nL,
                                                int lane, float inv, ConnState& cs, Counters& cnt) {
   const int wE = wave_max(nE), wL = wave_max(nL);
@@ -416,7 +420,7 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
     int kind = CONN_NONE;
     Conn cn;
     if (active) {
-      kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre);
+      kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre, EXT && STATS ? &cnt : nullptr);
       if (kind == CONN_DIRECT) {
 #if BDPT_DIRECT_LDS
         // straight into this lane's accumulator in the wave's LDS (only this wave writes it, and
@@ -458,7 +462,7 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
 #endif
     }
   };
-#if BDPT_CONN_COMPACT
+  if constexpr (COMPACT) {
   // The special strategies wave-uniformly: s = 0 (j = 0), the fresh light sample (j = 1),
   // light tracing to the camera (i = 1, j >= 2) ...
   for (int i = 2; i < wE; i++) conn_step(i, 0, i < nE);
@@ -481,7 +485,8 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
       if (jm == 0) { mE &= mE - 1; jm = mL; }
     }
   }
-#elif BDPT_CONN_ORDER == 1
+  } else {
+#if BDPT_CONN_ORDER == 1
   // E[i] loaded once per i and kept in registers across the j loop
   for (int i = 1; i < wE; i++) {
     const Vtx ev = PP.e(i >= 2 ? i : 2);
@@ -498,6 +503,7 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
   for (int i = 1; i < wE; i++)
     for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
 #endif
+  }
 #ifdef BDPT_PHASE_PROF
   cs.ph_gen += __builtin_amdgcn_s_memtime() - tg0;
 #endif
@@ -527,11 +533,13 @@ __device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const I
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const KParams& kp, int lane, unsigned nsamp, const Counters& cnt) {
   if (STATS) {
-    unsigned v[8] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes};
+    // slots 0..7 the scene counters, 12..14 the environment-table reads (8..11: phase profile)
+    unsigned v[11] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes,
+                      cnt.env_s, cnt.env_l, cnt.env_p};
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < 11; k++) {
       unsigned s = wave_sum(v[k]);
-      if (lane == 0 && s) atomicAdd(kp.stats + k, (unsigned long long)s);
+      if (lane == 0 && s) atomicAdd(kp.stats + (k < 8 ? k : k + 4), (unsigned long long)s);
     }
   }
 }
@@ -585,7 +593,7 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
 #ifdef BDPT_PHASE_PROF
       ph_prep += tp1 - tp0;
 #endif
-      connect_sample<LM, EXT>(kp, q, PathsInRegs<MAXV>(P), g, nE, nL, lane, inv, cs, cnt);
+      connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV>(P), g, nE, nL, lane, inv, cs, cnt);
     }
     finish_item<LM>(kp, q, it, lane, cs, cnt);
 #ifdef BDPT_PHASE_PROF
@@ -1149,7 +1157,7 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  unsigned long long s[8];
+  unsigned long long s[16];
   HIPCHK(hipMemcpy(s, c->d_stats, sizeof s, hipMemcpyDeviceToHost));
   memset(out, 0, sizeof *out);
   out->samples = s[0];
@@ -1167,6 +1175,9 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   out->bvh_depth = (uint64_t)c->hs.depth;
   out->lds_node_visits = s[7];
   out->lds_mode = c->last_lm;
+  out->env_samples = s[12];
+  out->env_lookups = s[13];
+  out->env_pdf_lookups = s[14];
   return BDPT_OK;
 }
 

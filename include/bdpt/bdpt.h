@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 5
+#define BDPT_ABI_VERSION 6
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -185,6 +185,11 @@ typedef struct bdpt_stats {
   int32_t lds_mode;           /* 0 scene in HBM, 1 whole scene in LDS, 2 BFS treelet in LDS +
                                  HBM below it, 3 flat primitive list in LDS; -1 none yet     */
   int32_t reserved0;
+  /* ABI v6: environment-light table reads, counted like the scene reads above */
+  uint64_t env_samples;       /* importance-sampled directions: 2 guide cells + 2 CDF entries per
+                                 axis, the texel pdf, 4 texels (76 B)                          */
+  uint64_t env_lookups;       /* radiance lookups along a direction: 4 texels (48 B)          */
+  uint64_t env_pdf_lookups;   /* texel pdf lookups (4 B)                                      */
 } bdpt_stats;
 
 int bdpt_abi_version(void);

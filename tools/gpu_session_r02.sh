@@ -27,6 +27,12 @@ if [ "${PART:-a}" = a ]; then
   step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 tools/prof_render.py $NS
   step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 tools/prof_render.py $NS
   step traffic 60 python3 tools/pmc_traffic.py $OUT ns "CBlucy stand-in 1920x1080 s128 m5, one launch (tools/prof_render.py)"
+  # C2 (the verdict's second traffic case): same passes into their own directories
+  C2="CBspheres 480 360 128 5 1"
+  mkdir -p $OUT/c2
+  step pmc_fetch_c2 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c2/pmc_fetch -o run -- python3 tools/prof_render.py $C2
+  step pmc_write_c2 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/c2/pmc_write -o run -- python3 tools/prof_render.py $C2
+  step traffic_c2 60 python3 tools/pmc_traffic.py $OUT/c2 c2 "CBspheres 480x360 s128 m5, one launch (tools/prof_render.py)"
 fi
 if [ "${PART:-a}" = b ]; then
   step bench_c2 600 python bench.py --workload c2 --no-cpu-baseline
