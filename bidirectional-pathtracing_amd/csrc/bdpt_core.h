@@ -396,9 +396,11 @@ static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDT
 BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM == 0 || LM == 2); }
 // With leaf_prefetch: the first record of a leaf is loaded where the descent produces the leaf
 // reference (inside the node loop, or at a pop), not after the wave's node loop ends, so the lanes
-// that reach their leaf early have the fetch in flight while the others still descend.
+// that reach their leaf early have the fetch in flight while the others still descend. Measured
+// slower (Lucy stand-in 594 -> 567, C5-shaped 465 -> 449 Msamples/s: 12 more registers live across
+// the node loop, more spills there): off.
 #ifndef BDPT_LEAF_EARLY
-#define BDPT_LEAF_EARLY 1
+#define BDPT_LEAF_EARLY 0
 #endif
 BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY; }
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
