@@ -44,7 +44,9 @@ struct Ctx {
   float* d_eye = nullptr;
   float* d_light = nullptr;
   float* d_sample = nullptr;
-  unsigned long long* d_stats = nullptr;   // [0..6] counters, [8..10] phase cycles, [15] tickets
+  // [0..7] counters, [12..14] environment-table reads, [15] tickets, [16..31] phase profile
+  static constexpr int kStatSlots = 32;
+  unsigned long long* d_stats = nullptr;
   // Tile-block lists of bdpt_render: a ring of pinned staging + device buffers, each slot reused
   // only after the event recorded behind the launch that read it, so back-to-back tile renders
   // (raytrace_tile / raytrace_pixel callers) never wait for the GPU.

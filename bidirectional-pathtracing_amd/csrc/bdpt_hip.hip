@@ -533,7 +533,7 @@ __device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const I
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const KParams& kp, int lane, unsigned nsamp, const Counters& cnt) {
   if (STATS) {
-    // slots 0..7 the scene counters, 12..14 the environment-table reads (8..11: phase profile)
+    // slots 0..7 the scene counters, 12..14 the environment-table reads (15: tickets, 16..31: phase profile)
     unsigned v[11] = {nsamp, cnt.closest, cnt.shadow, cnt.nodes, cnt.tris, cnt.sphs, cnt.hits, cnt.lnodes,
                       cnt.env_s, cnt.env_l, cnt.env_p};
 #pragma unroll
@@ -569,6 +569,8 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   Paths<MAXV> P;
 #ifdef BDPT_PHASE_PROF
   unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
+  unsigned long long ph_walk_wave = 0, ph_walk_lane = 0;   // walk iterations: wave (max) / lane sums
+  unsigned long long ph_cells = 0, ph_pairs = 0;           // connection grid cells / (i, j) pairs
 #endif
   const int grp = blockIdx.x & 7;
   int cur = 0;   // wave-uniform: XCD groups exhausted so far
@@ -583,6 +585,9 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       Rng g;
       int nE = 0, nL = 0;
       PH_STAMP(tp0);
+#ifdef BDPT_PHASE_PROF
+      const uint32_t c0 = cnt.closest;
+#endif
       if (t < it.my_n) {
         prepare_sample<MAXV, LM, EXT>(kp.S, kp.sp, P, cnt, g, it.x, it.y, (uint32_t)(it.s0 + t));
         nE = P.nE;
@@ -592,6 +597,11 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
       PH_STAMP(tp1);
 #ifdef BDPT_PHASE_PROF
       ph_prep += tp1 - tp0;
+      const int wi = (int)(cnt.closest - c0);
+      ph_walk_wave += (unsigned)wave_max(wi);
+      ph_walk_lane += (unsigned)wi;
+      ph_cells += (unsigned)(max(wave_max(nE) - 1, 0) * wave_max(nL));
+      ph_pairs += (unsigned)(max(nE - 1, 0) * nL);
 #endif
       connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV>(P), g, nE, nL, lane, inv, cs, cnt);
     }
@@ -607,6 +617,16 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
     atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
     atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
+    atomicAdd((unsigned long long*)kp.prof + 4, ph_walk_wave);
+    atomicAdd((unsigned long long*)kp.prof + 6, ph_cells);
+  }
+  {
+    const unsigned long long wl = (unsigned long long)wave_sum((unsigned)ph_walk_lane);
+    const unsigned long long wp = (unsigned long long)wave_sum((unsigned)ph_pairs);
+    if (lane == 0) {
+      atomicAdd((unsigned long long*)kp.prof + 5, wl);
+      atomicAdd((unsigned long long*)kp.prof + 7, wp);
+    }
   }
 #endif
   flush_stats<STATS>(kp, lane, nsamp, cnt);
@@ -905,7 +925,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
       hipMalloc((void**)&c->d_sample, fb) != hipSuccess ||
       hipMalloc((void**)&c->d_count, c->npix * sizeof(int)) != hipSuccess ||
       hipMalloc((void**)&c->d_work8, 8 * 32 * sizeof(unsigned)) != hipSuccess ||
-      hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc((void**)&c->d_stats, Ctx::kStatSlots * sizeof(unsigned long long)) != hipSuccess) {
     g_err = "out of device memory";
     return fail(BDPT_E_NOMEM);
   }
@@ -920,7 +940,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if (hipMemsetAsync(c->d_eye, 0, fb, c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_light, 0, fb, c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_count, 0, c->npix * sizeof(int), c->stream) != hipSuccess ||
-      hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_stats, 0, Ctx::kStatSlots * sizeof(unsigned long long), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess) { g_err = "init sync failed"; return fail(BDPT_E_DEVICE); }
   *ctx_out = c;
   return BDPT_OK;
@@ -954,7 +974,7 @@ int bdpt_clear(void* ctx) {
   HIPCHK(hipMemsetAsync(c->d_eye, 0, fb, c->stream));
   HIPCHK(hipMemsetAsync(c->d_light, 0, fb, c->stream));
   HIPCHK(hipMemsetAsync(c->d_count, 0, c->npix * sizeof(int), c->stream));
-  HIPCHK(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, Ctx::kStatSlots * sizeof(unsigned long long), c->stream));
   return BDPT_OK;
 }
 
@@ -974,7 +994,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.eye = c->d_eye;
   kp.light = c->d_light;
   kp.stats = c->d_stats;
-  kp.prof = c->d_stats + 8;
+  kp.prof = c->d_stats + 16;
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   kp.nmat = (int)c->hs.mats.size();
   kp.item_lo = 0;
@@ -1187,7 +1207,7 @@ int bdpt_debug_counters(void* ctx, uint64_t* out16) {
   std::lock_guard<std::recursive_mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  HIPCHK(hipMemcpy(out16, c->d_stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out16, c->d_stats + 16, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return BDPT_OK;
 }
 

@@ -238,8 +238,9 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out);
 int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, float* out_t,
                     int32_t* out_prim);
 
-/* Diagnostic hook: raw device counters (8 stats words + 8 phase-cycle words of a
- * BDPT_PHASE_PROF build). Sync. */
+/* Diagnostic hook: the 16 phase-profile words of a BDPT_PHASE_PROF build (cycles of the walks,
+ * connection generation and connection rays, walk traversal; walk iterations per wave / per lane;
+ * connection-grid cells / pairs). Sync. */
 int bdpt_debug_counters(void* ctx, uint64_t* out16);
 
 /* Host-side COLLADA loader: the reference CLI's scene path (ColladaParser::load,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run; no tracing domains combined with --pmc).
 cd "$(dirname "$0")/.." || exit 1
-OUT=gpurun_out/pmc
+OUT=gpurun_out/${PMC_TAG:-pmc}
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
@@ -23,5 +23,6 @@ FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
 GRBM_GUI_ACTIVE SQ_INSTS_FLAT SQ_INSTS_SCRATCH
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS
 GROUPS
 echo "== done"

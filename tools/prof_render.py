@@ -43,11 +43,15 @@ if os.environ.get("BDPT_PHASES"):
     arr = (C.c_uint64 * 16)()
     pt.lib.bdpt_debug_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     pt.lib.bdpt_debug_counters(pt.ctx, arr)
-    tot = arr[8] + arr[9] + arr[10]
+    tot = arr[0] + arr[1] + arr[2]
     print("phase cycles (wave-summed): prepare %.3g (%.1f%%)  conn-gen %.3g (%.1f%%)  flush %.3g (%.1f%%)" % (
-        arr[8], 100 * arr[8] / tot, arr[9], 100 * arr[9] / tot, arr[10], 100 * arr[10] / tot))
+        arr[0], 100 * arr[0] / tot, arr[1], 100 * arr[1] / tot, arr[2], 100 * arr[2] / tot))
     print("  of prepare: walk closest-hit traversal %.1f%% (wave-summed, divergent lanes counted once)" % (
-        100 * arr[11] / max(1, arr[8])))
+        100 * arr[3] / max(1, arr[0])))
+    print("  walk iterations: %.4g wave-level x 64 lanes, %.4g lane-level -> %.1f%% of the lane slots; "
+          "connection cells %.4g x 64, (i, j) pairs %.4g -> %.1f%%" % (
+              arr[4], arr[5], 100 * arr[5] / max(1, 64 * arr[4]), arr[6], arr[7],
+              100 * arr[7] / max(1, 64 * arr[6])))
 if os.environ.get("BDPT_STATS") == "1":
     st = pt.stats()
     n = max(1, st.samples)
