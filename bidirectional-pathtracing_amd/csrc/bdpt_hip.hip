@@ -186,7 +186,7 @@ struct SplatCache {
 // lane whose ray is done takes the next pending one (resumable any_step, bdpt_core.h), so the
 // wave's lanes stay busy until the queue runs dry instead of waiting for the slowest of 64 rays.
 #ifndef BDPT_FLUSH_REFILL
-#define BDPT_FLUSH_REFILL 0   // measured slower on the Cornell-box scenes (more spills)
+#define BDPT_FLUSH_REFILL 0   // 1: drain the whole ring (64..127 rays) with lane refill; measured -0.5% Lucy, -6% CBspheres
 #endif
 template <int LM>
 __device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int head, int tail, int lane, float* light,
@@ -394,6 +394,9 @@ __device__ __forceinline__ bool next_item(const KParams& kp, int lane, int grp, 
 struct ConnState {
   float dxs = 0, dys = 0, dzs = 0;
   int head = 0, tail = 0;
+#if BDPT_FLUSH_REFILL
+  SplatCache sc;   // flush_refill's per-lane light-image target, written out at the item's end
+#endif
 #ifdef BDPT_PHASE_PROF
   unsigned long long ph_gen = 0, ph_flush = 0;
 #endif
@@ -453,9 +456,16 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
       PH_STAMP(tp0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+#if BDPT_FLUSH_REFILL
+      // every queued ray (64..127), idle lanes refilled from the backlog
+      flush_refill<LM>(kp.S, q, cs.head, cs.tail, lane, kp.light, cnt, cs.sc);
+      __builtin_amdgcn_wave_barrier();
+      cs.head = cs.tail;
+#else
       flush_queue<LM>(kp.S, q, cs.head, 64, lane, kp.light, cnt);
       __builtin_amdgcn_wave_barrier();
       cs.head += 64;
+#endif
       PH_STAMP(tp1);
 #ifdef BDPT_PHASE_PROF
       cs.ph_flush += tp1 - tp0;
@@ -516,8 +526,15 @@ __device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const I
   if (cs.tail > cs.head) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+#if BDPT_FLUSH_REFILL
+    flush_refill<LM>(kp.S, q, cs.head, cs.tail, lane, kp.light, cnt, cs.sc);
+#else
     flush_queue<LM>(kp.S, q, cs.head, cs.tail - cs.head, lane, kp.light, cnt);
+#endif
   }
+#if BDPT_FLUSH_REFILL
+  cs.sc.flush(kp.light, lane);
+#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (it.my_n > 0) {
