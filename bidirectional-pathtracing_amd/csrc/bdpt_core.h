@@ -273,6 +273,8 @@ struct Counters {
   uint32_t env_s = 0, env_l = 0, env_p = 0;   // environment-light samples / radiance / pdf lookups
 #ifdef BDPT_PHASE_PROF
   unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
+  unsigned long long clk_light = 0;        // ... drawing the light vertex L[1] (sample_light_ray)
+  unsigned long long clk_vertex = 0;       // ... from a hit to the next ray (shading record, vertex, sample_f)
 #endif
 };
 
@@ -379,9 +381,13 @@ namespace bdpt {
 #endif
 static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
               "BVH widths must be 2 or 4");
-// Any-hit (connection-ray) traversal order: 0 = children in slot order, 1 = near-first like closest hit
+// Child visiting order of the 4-wide node step: 0 = slot order, 1 = near-first (sorting network),
+// 2 = the nearest first, the others in slot order. Any hit (connection rays): 0; closest hit: 1.
 #ifndef BDPT_ANY_ORD
 #define BDPT_ANY_ORD 0
+#endif
+#ifndef BDPT_CLOSEST_ORD
+#define BDPT_CLOSEST_ORD 1
 #endif
 // LM 3: walk the flat list as one run of primitives with the next record prefetched (S.fn > 0)
 #ifndef BDPT_FLAT_PREFETCH
@@ -547,7 +553,7 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
 // Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad
 // ORD: visit hit children near-first (closest-hit queries); any-hit queries take them in slot order.
 // A child is entered when its slab interval, clipped to [tmin, tmax], is non-empty.
-template <int K, int LM, bool ORD = true>
+template <int K, int LM, int ORD = 1>
 BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
                       Counters& c) {
   constexpr int W = lm_width(LM), NU = node_used_f4(W);
@@ -573,7 +579,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     const bool hr = fmaxf(tnr, tmin) <= fminf(tfr, tmax);
     const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
     if (hl && hr) {
-      const bool lfirst = !ORD || tnl <= tnr;
+      const bool lfirst = ORD == 0 || tnl <= tnr;
       stk.push(lfirst ? rref : lref);
       return lfirst ? lref : rref;
     }
@@ -599,7 +605,23 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
       slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
       h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
     }
-    if (!ORD) {
+    if (ORD == 2) {
+      // continue with the nearest hit child, push the others in slot order (no sorting network)
+      const float k0 = h0 ? tn0 : INFINITY, k1 = h1 ? tn1 : INFINITY, k2 = h2 ? tn2 : INFINITY, k3 = h3 ? tn3 : INFINITY;
+      const float m01 = fminf(k0, k1), m23 = fminf(k2, k3);
+      const float mn = fminf(m01, m23);
+      if (!(mn < INFINITY)) {
+        int nx;
+        return stk.pop(nx) ? nx : kTravDone;
+      }
+      const int best = mn == k0 ? 0 : mn == k1 ? 1 : mn == k2 ? 2 : 3;
+      if (h3 && best != 3) stk.push(r3);
+      if (h2 && best != 2) stk.push(r2);
+      if (h1 && best != 1) stk.push(r1);
+      if (h0 && best != 0) stk.push(r0);
+      return best == 0 ? r0 : best == 1 ? r1 : best == 2 ? r2 : r3;
+    }
+    if (ORD == 0) {
       // continue with the lowest hit slot, push the others
       int nx = kTravDone;
       if (h3) nx = r3;
@@ -688,7 +710,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       ref = ld_lds_i(S.lleaves + li++);
     }
     while (ref >= 0) {
-      ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
+      ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
       if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
     }
     if (ref == kTravDone) break;
@@ -782,7 +804,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       ref = ld_lds_i(S.lleaves + li++);
     }
     while (ref >= 0) {
-      ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
+      ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
       if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
     }
     if (ref == kTravDone) return false;
@@ -827,7 +849,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
 template <int LM, int K>
 BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
                                              int& ref, TravStack<K>& stk, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM>(S, r, ref, tmin, h.t, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
   if (ref == kTravDone) return true;
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -856,7 +878,7 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
 template <int LM, int K>
 BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
                                          int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD != 0>(S, r, ref, tmin, tmax, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
   if (ref == kTravDone) { *hit = false; return true; }
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -1639,7 +1661,13 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   Rng gl0 = g;
   f3 lo, ld, ln, la1;
   float ldp;
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+#endif
   sample_light(gl0, lo, ld, ln, la1, ldp);
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  cnt.clk_light += __builtin_amdgcn_s_memtime() - tl0;
+#endif
   const uint32_t lpos = gl0.pos;
 #if BDPT_LATE_LIGHT == 2
   P.l1_d = ld;
@@ -1673,7 +1701,8 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
 #endif
     bool end = !trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    cnt.clk_walk_trace += __builtin_amdgcn_s_memtime() - tq0;
+    const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
+    cnt.clk_walk_trace += tq1 - tq0;
 #endif
     if (EXT && end && !light && S.env.light >= 0) {
       // an escaped eye ray ends on the environment light: vertex at infinity in direction rd
@@ -1774,6 +1803,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         nalpha = next_alpha(v.alpha, n, rd, fv, pdf * q);
         i++;
       }
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+      cnt.clk_vertex += __builtin_amdgcn_s_memtime() - tq1;
+#endif
     }
     if (end) {
       if (light) {

@@ -636,6 +636,8 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
     atomicAdd((unsigned long long*)kp.prof + 4, ph_walk_wave);
     atomicAdd((unsigned long long*)kp.prof + 6, ph_cells);
+    atomicAdd((unsigned long long*)kp.prof + 8, cnt.clk_light);
+    atomicAdd((unsigned long long*)kp.prof + 9, cnt.clk_vertex);
   }
   {
     const unsigned long long wl = (unsigned long long)wave_sum((unsigned)ph_walk_lane);

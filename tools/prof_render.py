@@ -48,6 +48,8 @@ if os.environ.get("BDPT_PHASES"):
         arr[0], 100 * arr[0] / tot, arr[1], 100 * arr[1] / tot, arr[2], 100 * arr[2] / tot))
     print("  of prepare: walk closest-hit traversal %.1f%% (wave-summed, divergent lanes counted once)" % (
         100 * arr[3] / max(1, arr[0])))
+    print("  of prepare: light vertex L[1] %.1f%%, hit -> next ray (shading, vertex, sample_f) %.1f%%" % (
+        100 * arr[8] / max(1, arr[0]), 100 * arr[9] / max(1, arr[0])))
     print("  walk iterations: %.4g wave-level x 64 lanes, %.4g lane-level -> %.1f%% of the lane slots; "
           "connection cells %.4g x 64, (i, j) pairs %.4g -> %.1f%%" % (
               arr[4], arr[5], 100 * arr[5] / max(1, 64 * arr[4]), arr[6], arr[7],
