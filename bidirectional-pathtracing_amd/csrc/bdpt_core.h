@@ -409,6 +409,26 @@ BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM 
 #define BDPT_LEAF_EARLY 0
 #endif
 BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY; }
+// Speculative while-while (Aila & Laine 2009; trace_closest / trace_any): a lane holding a
+// postponed leaf keeps descending while other lanes still look for theirs. Where the nodes come from
+// HBM (LM 0 / 2) the extra node steps fill the lanes that would otherwise wait: Lucy stand-in 601 ->
+// 631, C5-shaped 468 -> 485 Msamples/s; with the whole tree in LDS (LM 1) the longer steps cost
+// more than the latency they hide (CBgems m7 269 -> 247), so only LM 0 / 2.
+#ifndef BDPT_SPEC
+#define BDPT_SPEC 1
+#endif
+BDPT_HD constexpr bool spec_trav(int LM) { return BDPT_SPEC && (LM == 0 || LM == 2); }
+#ifndef BDPT_SPEC_ANY
+#define BDPT_SPEC_ANY 1   // connection rays too (Lucy stand-in +0.6% over closest hit alone)
+#endif
+// true if the predicate holds on any active lane of the wave (the host build runs one lane)
+BDPT_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(p) != 0;
+#else
+  return p;
+#endif
+}
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
@@ -703,18 +723,9 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     const int s3 = 3 * leaf_start(lr);
     a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
   };
-  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-  for (;;) {
-    if (LM == 3) {
-      if (li >= S.nleaves) break;
-      ref = ld_lds_i(S.lleaves + li++);
-    }
-    while (ref >= 0) {
-      ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
-      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-    }
-    if (ref == kTravDone) break;
-    const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  // the primitives of leaf lf, closest hit so far in h
+  auto test_leaf = [&](int lf) {
+    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
@@ -755,8 +766,46 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
       }
     }
+  };
+  if constexpr (spec_trav(LM)) {
+    // speculative while-while: a lane's first leaf is postponed and the lane goes on descending its
+    // stack while other lanes still look for theirs; leaves are tested once every lane has one
+    int pend = 0;
+    for (;;) {
+      while (ref >= 0) {
+        ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
+        if (ref < 0 && ref != kTravDone && pend == 0) {
+          pend = ref;
+          if (!stk.pop(ref)) ref = kTravDone;
+        }
+        if (!wave_any(pend == 0 && ref >= 0)) break;
+      }
+      while (pend != 0) {
+        test_leaf(pend);
+        pend = 0;
+        if (ref < 0 && ref != kTravDone) {
+          pend = ref;
+          if (!stk.pop(ref)) ref = kTravDone;
+        }
+      }
+      if (ref == kTravDone) break;
+    }
+  } else {
+  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+  for (;;) {
+    if (LM == 3) {
+      if (li >= S.nleaves) break;
+      ref = ld_lds_i(S.lleaves + li++);
+    }
+    while (ref >= 0) {
+      ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
+      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+    }
+    if (ref == kTravDone) break;
+    test_leaf(ref);
     if (LM != 3 && !stk.pop(ref)) break;
     if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
+  }
   }
   if (h.prim >= 0) c.hits++;
   return h.prim >= 0;
@@ -797,18 +846,9 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     const int s3 = 3 * leaf_start(lr);
     a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
   };
-  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-  for (;;) {
-    if (LM == 3) {
-      if (li >= S.nleaves) return false;
-      ref = ld_lds_i(S.lleaves + li++);
-    }
-    while (ref >= 0) {
-      ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
-      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-    }
-    if (ref == kTravDone) return false;
-    const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
+  // true if a primitive of leaf lf is hit on [tmin, tmax]
+  auto test_leaf = [&](int lf) -> bool {
+    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
@@ -838,8 +878,46 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       }
       if (ok) return true;
     }
+    return false;
+  };
+  if constexpr (spec_trav(LM) && BDPT_SPEC_ANY) {
+    // speculative while-while, as in trace_closest
+    int pend = 0;
+    for (;;) {
+      while (ref >= 0) {
+        ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
+        if (ref < 0 && ref != kTravDone && pend == 0) {
+          pend = ref;
+          if (!stk.pop(ref)) ref = kTravDone;
+        }
+        if (!wave_any(pend == 0 && ref >= 0)) break;
+      }
+      while (pend != 0) {
+        if (test_leaf(pend)) return true;
+        pend = 0;
+        if (ref < 0 && ref != kTravDone) {
+          pend = ref;
+          if (!stk.pop(ref)) ref = kTravDone;
+        }
+      }
+      if (ref == kTravDone) return false;
+    }
+  } else {
+  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+  for (;;) {
+    if (LM == 3) {
+      if (li >= S.nleaves) return false;
+      ref = ld_lds_i(S.lleaves + li++);
+    }
+    while (ref >= 0) {
+      ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
+      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
+    }
+    if (ref == kTravDone) return false;
+    if (test_leaf(ref)) return true;
     if (LM != 3 && !stk.pop(ref)) return false;
     if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
+  }
   }
 }
 
