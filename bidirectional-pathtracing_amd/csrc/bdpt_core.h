@@ -417,16 +417,26 @@ BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEA
 #ifndef BDPT_SPEC
 #define BDPT_SPEC 1
 #endif
-BDPT_HD constexpr bool spec_trav(int LM) { return BDPT_SPEC && (LM == 0 || LM == 2); }
+#ifndef BDPT_SPEC_LM1
+#define BDPT_SPEC_LM1 0
+#endif
+BDPT_HD constexpr bool spec_trav(int LM) { return BDPT_SPEC && (LM == 0 || LM == 2 || (LM == 1 && BDPT_SPEC_LM1)); }
 #ifndef BDPT_SPEC_ANY
 #define BDPT_SPEC_ANY 1   // connection rays too (Lucy stand-in +0.6% over closest hit alone)
 #endif
-// true if the predicate holds on any active lane of the wave (the host build runs one lane)
-BDPT_HD bool wave_any(bool p) {
+// The descent stops once fewer than BDPT_SPEC_MIN lanes still look for their first leaf (1: once
+// all have one); the others go on after the leaf tests. Measured on the Lucy stand-in: 1 630, 4 574,
+// 8 523, 16 491 Msamples/s (stragglers then descend alone); speculation in the LDS-resident tree
+// (BDPT_SPEC_LM1) with 8: CBgems m7 269 -> 201.
+#ifndef BDPT_SPEC_MIN
+#define BDPT_SPEC_MIN 1
+#endif
+// active lanes of the wave for which the predicate holds (the host build runs one lane)
+BDPT_HD int wave_count(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __ballot(p) != 0;
+  return __popcll(__ballot(p));
 #else
-  return p;
+  return p ? 1 : 0;
 #endif
 }
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
@@ -778,7 +788,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-        if (!wave_any(pend == 0 && ref >= 0)) break;
+        if (wave_count(pend == 0 && ref >= 0) < BDPT_SPEC_MIN) break;
       }
       while (pend != 0) {
         test_leaf(pend);
@@ -890,7 +900,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-        if (!wave_any(pend == 0 && ref >= 0)) break;
+        if (wave_count(pend == 0 && ref >= 0) < BDPT_SPEC_MIN) break;
       }
       while (pend != 0) {
         if (test_leaf(pend)) return true;
