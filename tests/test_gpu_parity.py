@@ -406,3 +406,18 @@ def test_concurrent_tile_callers():
         pt.close()
     assert _rmse(eye[60, 40:48], full["eye"][60, 40:48]) < RMSE_TOL
     assert np.count_nonzero(eye.sum(axis=2)) <= 8
+
+
+def test_env_table_read_counters():
+    """bdpt_stats v6: the environment-table reads the bench adds to the algorithmic bytes are
+    counted in scenes with an environment light (a direction sampled for some light vertices and
+    for the fresh light sample of (i, 1) connections; radiance lookups for escaped eye rays, with a
+    pdf lookup for each that carries a contribution) and are zero without one."""
+    W, H, S, M = 96, 72, 2, 8
+    sc = golden_scene("CBspheres_lambertian", W, H)
+    st0 = _gpu_render(sc, W, H, S, M, stats=True)["stats"]
+    assert (st0.env_samples, st0.env_lookups, st0.env_pdf_lookups) == (0, 0, 0)
+    st = _gpu_render(_with_env(sc), W, H, S, M, stats=True, rr=True)["stats"]
+    assert st.samples == W * H * S
+    assert st.env_samples > 0 and st.env_lookups > 0
+    assert 0 < st.env_pdf_lookups <= st.env_lookups
