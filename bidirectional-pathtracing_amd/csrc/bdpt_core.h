@@ -41,6 +41,7 @@ struct float4 {
   float x, y, z, w;
 };
 inline int __float_as_int(float f) { int i; std::memcpy(&i, &f, 4); return i; }
+inline float __int_as_float(int i) { float f; std::memcpy(&f, &i, 4); return f; }
 #endif
 
 namespace bdpt {
@@ -445,8 +446,23 @@ BDPT_HD int wave_count(bool p) {
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
-BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
-BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
+// 4-wide nodes with quantized child boxes (64 B instead of 128 B): the parent's fp32 origin and a
+// power-of-two step per axis, each child plane an 8-bit multiple of the step rounded outward, so a
+// decoded box contains the padded fp32 box (checked exactly when the host emits it). Half the
+// node bytes: twice the treelet in the same LDS, half the L2 / Infinity-Cache footprint.
+#ifndef BDPT_QNODE
+#define BDPT_QNODE 0
+#endif
+// 4-wide fp32 nodes: the slab planes as packed fmas (v_pk_fma_f32, two children per instruction)
+#ifndef BDPT_PK_SLAB
+#define BDPT_PK_SLAB 0
+#endif
+// LM 2 node fetches: wave-uniform LDS-only / HBM-only paths, mixed waves fetch both (node_step)
+#ifndef BDPT_NODE_SPLIT
+#define BDPT_NODE_SPLIT 0
+#endif
+BDPT_HD constexpr int node_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 8) : 4; }        // float4 per node (stride)
+BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 7) : 4; }   // float4 a traversal reads
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
@@ -551,7 +567,7 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)p;
   v4f t[7];
-  if (W == 4) {
+  if (node_used_f4(W) == 7) {
     asm volatile(
         "ds_read_b128 %0, %7\n\t"
         "ds_read_b128 %1, %7 offset:16\n\t"
@@ -595,6 +611,32 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
     c.lnodes += W;
+  } else if (LM == 2 && BDPT_NODE_SPLIT) {
+    // Treelet (LDS) and HBM lanes in one wave: a lane-divergent if / else over the same registers
+    // runs the global loads, waits for them (the ds_reads would overwrite their registers), then
+    // the ds_reads — HBM latency + LDS latency. Here the wave takes one path when all its lanes
+    // agree; a mixed wave issues both fetches into separate registers (every lane reads LDS and
+    // HBM, the treelet nodes are in both) and selects, so the two latencies overlap.
+    const bool in_lds = ref < S.ntop;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t ml = __ballot(in_lds), ma = __ballot(true);
+#else
+    const uint64_t ml = in_lds ? 1u : 0u, ma = 1u;
+#endif
+    if (in_lds) c.lnodes += W;
+    if (ml == ma) {
+      ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
+    } else if (ml == 0) {
+#pragma unroll
+      for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
+    } else {
+      float4 tl[NU];
+#pragma unroll
+      for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
+      ld_node_lds<W>(S.lnodes + node_f4(W) * (in_lds ? ref : 0), tl);
+#pragma unroll
+      for (int k = 0; k < NU; k++) v[k] = in_lds ? tl[k] : v[k];
+    }
   } else if (LM == 2 && ref < S.ntop) {
     ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
     c.lnodes += W;
@@ -621,12 +663,73 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     int nx;
     return stk.pop(nx) ? nx : kTravDone;
   } else {
-    const float4 lx = v[0], hx = v[1], ly = v[2 % NU], hy = v[3 % NU];
-    const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
     c.nodes += 4;
-    int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y), r2 = __float_as_int(e.z), r3 = __float_as_int(e.w);
+    int r0, r1, r2, r3;
     float tn0, tn1, tn2, tn3;
     bool h0, h1, h2, h3;
+    if (BDPT_QNODE) {
+      // (o.x, o.y, o.z, biased exponents) | lo.x hi.x lo.y hi.y | lo.z hi.z ref0 ref1 | ref2 ref3 -,
+      // each plane word = four children's bytes. Plane p = o + q * 2^e, so its slab distance is
+      // fma(q, 2^e * inv, (o - ray.o) * inv): q * (2^e * inv) is exact, one rounding more than the
+      // fp32 box form, covered by the same 2^-16 padding the decoded box contains.
+      const float4 q0 = v[0], q1 = v[1 % NU], q2 = v[2 % NU], q3 = v[3 % NU];
+      const uint32_t ex = (uint32_t)__float_as_int(q0.w);
+      const float ax = __int_as_float((int)((ex & 0xffu) << 23)) * r.inv.x;
+      const float ay = __int_as_float((int)(((ex >> 8) & 0xffu) << 23)) * r.inv.y;
+      const float az = __int_as_float((int)(((ex >> 16) & 0xffu) << 23)) * r.inv.z;
+      const float bx = fmaf(q0.x, r.inv.x, -r.oi.x), by = fmaf(q0.y, r.inv.y, -r.oi.y), bz = fmaf(q0.z, r.inv.z, -r.oi.z);
+      const uint32_t wlx = (uint32_t)__float_as_int(q1.x), whx = (uint32_t)__float_as_int(q1.y);
+      const uint32_t wly = (uint32_t)__float_as_int(q1.z), why = (uint32_t)__float_as_int(q1.w);
+      const uint32_t wlz = (uint32_t)__float_as_int(q2.x), whz = (uint32_t)__float_as_int(q2.y);
+      r0 = __float_as_int(q2.z); r1 = __float_as_int(q2.w); r2 = __float_as_int(q3.x); r3 = __float_as_int(q3.y);
+      auto qslab = [&](int sh, float* tn) {   // child in byte sh/8 of every plane word
+        const float t0x = fmaf((float)((wlx >> sh) & 0xffu), ax, bx), t1x = fmaf((float)((whx >> sh) & 0xffu), ax, bx);
+        const float t0y = fmaf((float)((wly >> sh) & 0xffu), ay, by), t1y = fmaf((float)((why >> sh) & 0xffu), ay, by);
+        const float t0z = fmaf((float)((wlz >> sh) & 0xffu), az, bz), t1z = fmaf((float)((whz >> sh) & 0xffu), az, bz);
+        *tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        return fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)) * 1.00000024f;
+      };
+      float tf;
+      tf = qslab(0, &tn0);
+      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
+      tf = qslab(8, &tn1);
+      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
+      tf = qslab(16, &tn2);
+      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
+      tf = qslab(24, &tn3);
+      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
+    } else {
+    const float4 lx = v[0], hx = v[1], ly = v[2 % NU], hy = v[3 % NU];
+    const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
+    r0 = __float_as_int(e.x); r1 = __float_as_int(e.y); r2 = __float_as_int(e.z); r3 = __float_as_int(e.w);
+#if defined(__HIP_DEVICE_COMPILE__) && BDPT_PK_SLAB
+    if (true) {
+      // the 24 slab planes as 12 packed fmas (v_pk_fma_f32: two children per instruction; the same
+      // fused result per element as slab()), then slab()'s min / max per child
+      typedef float v2f __attribute__((ext_vector_type(2)));
+      const v2f ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
+      const v2f mx = {-r.oi.x, -r.oi.x}, my = {-r.oi.y, -r.oi.y}, mz = {-r.oi.z, -r.oi.z};
+      const v2f lx01 = __builtin_elementwise_fma((v2f){lx.x, lx.y}, ix, mx), lx23 = __builtin_elementwise_fma((v2f){lx.z, lx.w}, ix, mx);
+      const v2f hx01 = __builtin_elementwise_fma((v2f){hx.x, hx.y}, ix, mx), hx23 = __builtin_elementwise_fma((v2f){hx.z, hx.w}, ix, mx);
+      const v2f ly01 = __builtin_elementwise_fma((v2f){ly.x, ly.y}, iy, my), ly23 = __builtin_elementwise_fma((v2f){ly.z, ly.w}, iy, my);
+      const v2f hy01 = __builtin_elementwise_fma((v2f){hy.x, hy.y}, iy, my), hy23 = __builtin_elementwise_fma((v2f){hy.z, hy.w}, iy, my);
+      const v2f lz01 = __builtin_elementwise_fma((v2f){lz.x, lz.y}, iz, mz), lz23 = __builtin_elementwise_fma((v2f){lz.z, lz.w}, iz, mz);
+      const v2f hz01 = __builtin_elementwise_fma((v2f){hz.x, hz.y}, iz, mz), hz23 = __builtin_elementwise_fma((v2f){hz.z, hz.w}, iz, mz);
+      auto fin = [&](float t0x, float t1x, float t0y, float t1y, float t0z, float t1z, float* tn) {
+        *tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+        return fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)) * 1.00000024f;
+      };
+      float tf;
+      tf = fin(lx01.x, hx01.x, ly01.x, hy01.x, lz01.x, hz01.x, &tn0);
+      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
+      tf = fin(lx01.y, hx01.y, ly01.y, hy01.y, lz01.y, hz01.y, &tn1);
+      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
+      tf = fin(lx23.x, hx23.x, ly23.x, hy23.x, lz23.x, hz23.x, &tn2);
+      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
+      tf = fin(lx23.y, hx23.y, ly23.y, hy23.y, lz23.y, hz23.y, &tn3);
+      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
+    } else
+#endif
     {
       float tf;
       slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn0, &tf);
@@ -637,6 +740,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
       h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
       slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
       h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
+    }
     }
     if (ORD == 2) {
       // continue with the nearest hit child, push the others in slot order (no sorting network)
