@@ -459,7 +459,7 @@ BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BV
 #endif
 // LM 2 node fetches: wave-uniform LDS-only / HBM-only paths, mixed waves fetch both (node_step)
 #ifndef BDPT_NODE_SPLIT
-#define BDPT_NODE_SPLIT 0
+#define BDPT_NODE_SPLIT 1
 #endif
 BDPT_HD constexpr int node_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 8) : 4; }        // float4 per node (stride)
 BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 7) : 4; }   // float4 a traversal reads
@@ -596,6 +596,46 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
 #endif
 }
 
+// A node from HBM as one asm block of global loads and its own wait (BDPT_NODE_SPLIT 2): nothing
+// is left in flight into the registers the LDS path's ds_reads write, so the compiler puts no
+// vmcnt wait (for these loads, or for unrelated scratch stores) in front of those ds_reads.
+template <int W>
+BDPT_HD void ld_node_glb(const float4* p, float4* v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(1))) float4* g = (const __attribute__((address_space(1))) float4*)p;
+  v4f t[7];
+  if (node_used_f4(W) == 7) {
+    asm volatile(
+        "global_load_dwordx4 %0, %7, off\n\t"
+        "global_load_dwordx4 %1, %7, off offset:16\n\t"
+        "global_load_dwordx4 %2, %7, off offset:32\n\t"
+        "global_load_dwordx4 %3, %7, off offset:48\n\t"
+        "global_load_dwordx4 %4, %7, off offset:64\n\t"
+        "global_load_dwordx4 %5, %7, off offset:80\n\t"
+        "global_load_dwordx4 %6, %7, off offset:96\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
+        : "v"(g)
+        );
+  } else {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off\n\t"
+        "global_load_dwordx4 %1, %4, off offset:16\n\t"
+        "global_load_dwordx4 %2, %4, off offset:32\n\t"
+        "global_load_dwordx4 %3, %4, off offset:48\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+        : "v"(g)
+        );
+  }
+#pragma unroll
+  for (int k = 0; k < node_used_f4(W); k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
+#else
+  for (int k = 0; k < node_used_f4(W); k++) v[k] = p[k];
+#endif
+}
+
 // One node of the descent: slab-test the children, continue with the nearest hit child, push the
 // other hit children (farther first, so they pop near-first); pop when none is hit.
 // Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
@@ -614,28 +654,23 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
   } else if (LM == 2 && BDPT_NODE_SPLIT) {
     // Treelet (LDS) and HBM lanes in one wave: a lane-divergent if / else over the same registers
     // runs the global loads, waits for them (the ds_reads would overwrite their registers), then
-    // the ds_reads — HBM latency + LDS latency. Here the wave takes one path when all its lanes
-    // agree; a mixed wave issues both fetches into separate registers (every lane reads LDS and
-    // HBM, the treelet nodes are in both) and selects, so the two latencies overlap.
+    // the ds_reads — HBM latency + LDS latency. Here only a wave whose lanes are all in the treelet
+    // reads LDS; any other wave fetches every lane's node from HBM (the treelet nodes are there too,
+    // and hot in L2), one fetch latency either way.
     const bool in_lds = ref < S.ntop;
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint64_t ml = __ballot(in_lds), ma = __ballot(true);
+    const bool all_lds = __ballot(in_lds) == __ballot(true);
 #else
-    const uint64_t ml = in_lds ? 1u : 0u, ma = 1u;
+    const bool all_lds = in_lds;
 #endif
-    if (in_lds) c.lnodes += W;
-    if (ml == ma) {
+    if (all_lds) {
       ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
-    } else if (ml == 0) {
-#pragma unroll
-      for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
+      c.lnodes += W;
+    } else if (BDPT_NODE_SPLIT == 2) {
+      ld_node_glb<W>(S.nodes + node_f4(W) * ref, v);
     } else {
-      float4 tl[NU];
 #pragma unroll
       for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
-      ld_node_lds<W>(S.lnodes + node_f4(W) * (in_lds ? ref : 0), tl);
-#pragma unroll
-      for (int k = 0; k < NU; k++) v[k] = in_lds ? tl[k] : v[k];
     }
   } else if (LM == 2 && ref < S.ntop) {
     ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
