@@ -7,7 +7,7 @@
 # offset and the process crashed on its way out).
 cd "$(dirname "$0")/.." || exit 1
 CS=bidirectional-pathtracing_amd/csrc
-FL="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -Iinclude -I$CS"
+FL="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -fPIC -Iinclude -I$CS"
 UNITS="bdpt_hip.hip bdpt_wavefront.hip bdpt_scene.cpp dae_loader.cpp exr_loader.cpp"
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
