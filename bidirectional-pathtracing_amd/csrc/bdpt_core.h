@@ -409,7 +409,7 @@ BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM 
 #ifndef BDPT_LEAF_EARLY
 #define BDPT_LEAF_EARLY 0
 #endif
-BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY; }
+
 // Speculative while-while (Aila & Laine 2009; trace_closest / trace_any): a lane holding a
 // postponed leaf keeps descending while other lanes still look for theirs. Where the nodes come from
 // HBM (LM 0 / 2) the extra node steps fill the lanes that would otherwise wait: Lucy stand-in 601 ->
@@ -422,6 +422,9 @@ BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEA
 #define BDPT_SPEC_LM1 0
 #endif
 BDPT_HD constexpr bool spec_trav(int LM) { return BDPT_SPEC && (LM == 0 || LM == 2 || (LM == 1 && BDPT_SPEC_LM1)); }
+// leaf_early only in the plain while-while loops: the speculative loops produce and postpone leaves
+// without fetching their first record, so test_leaf must load it there (results would be wrong).
+BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY && !spec_trav(LM); }
 #ifndef BDPT_SPEC_TWO
 #define BDPT_SPEC_TWO 0   // up to two postponed leaves per lane: measured -6% (Lucy stand-in), -4% C5-shaped
 #endif
