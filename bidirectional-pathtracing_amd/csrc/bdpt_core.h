@@ -382,62 +382,23 @@ namespace bdpt {
 #endif
 static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
               "BVH widths must be 2 or 4");
-// Child visiting order of the 4-wide node step: 0 = slot order, 1 = near-first (sorting network),
-// 2 = the nearest first, the others in slot order. Any hit (connection rays): 0; closest hit: 1.
-#ifndef BDPT_ANY_ORD
-#define BDPT_ANY_ORD 0
-#endif
-#ifndef BDPT_CLOSEST_ORD
-#define BDPT_CLOSEST_ORD 1
-#endif
-// LM 3: walk the flat list as one run of primitives with the next record prefetched (S.fn > 0)
-#ifndef BDPT_FLAT_PREFETCH
-#define BDPT_FLAT_PREFETCH 1
-#endif
-// BVH leaves: the next primitive's record loaded before the current one is tested, where the
+// Child visiting order of the 4-wide node step: 0 = slot order (any-hit connection rays),
+// 1 = near-first by a sorting network (closest-hit queries).
+constexpr int kAnyOrd = 0, kClosestOrd = 1;
+// BVH leaves: the next primitive's record is loaded before the current one is tested, where the
 // geometry comes from HBM (LM 0 / 2). Measured: Lucy stand-in 1080p 489 -> 516, CBbunny 800x600
-// 351 -> 370 Msamples/s; with the geometry in LDS (LM 1, CBgems) 303 -> 299, so off there.
-#ifndef BDPT_LEAF_PREFETCH
-#define BDPT_LEAF_PREFETCH 1
-#endif
-BDPT_HD constexpr bool leaf_prefetch(int LM) { return BDPT_LEAF_PREFETCH && (LM == 0 || LM == 2); }
-// With leaf_prefetch: the first record of a leaf is loaded where the descent produces the leaf
-// reference (inside the node loop, or at a pop), not after the wave's node loop ends, so the lanes
-// that reach their leaf early have the fetch in flight while the others still descend. Measured
-// slower (Lucy stand-in 594 -> 567, C5-shaped 465 -> 449 Msamples/s: 12 more registers live across
-// the node loop, more spills there): off.
-#ifndef BDPT_LEAF_EARLY
-#define BDPT_LEAF_EARLY 0
-#endif
+// 351 -> 370 Msamples/s; with the geometry in LDS (LM 1, CBgems) 303 -> 299, so off there. LM 3
+// walks its flat list the same way (S.fn > 0).
+BDPT_HD constexpr bool leaf_prefetch(int LM) { return LM == 0 || LM == 2; }
 
 // Speculative while-while (Aila & Laine 2009; trace_closest / trace_any): a lane holding a
-// postponed leaf keeps descending while other lanes still look for theirs. Where the nodes come from
-// HBM (LM 0 / 2) the extra node steps fill the lanes that would otherwise wait: Lucy stand-in 601 ->
-// 631, C5-shaped 468 -> 485 Msamples/s; with the whole tree in LDS (LM 1) the longer steps cost
-// more than the latency they hide (CBgems m7 269 -> 247), so only LM 0 / 2.
-#ifndef BDPT_SPEC
-#define BDPT_SPEC 1
-#endif
-#ifndef BDPT_SPEC_LM1
-#define BDPT_SPEC_LM1 0
-#endif
-BDPT_HD constexpr bool spec_trav(int LM) { return BDPT_SPEC && (LM == 0 || LM == 2 || (LM == 1 && BDPT_SPEC_LM1)); }
-// leaf_early only in the plain while-while loops: the speculative loops produce and postpone leaves
-// without fetching their first record, so test_leaf must load it there (results would be wrong).
-BDPT_HD constexpr bool leaf_early(int LM) { return leaf_prefetch(LM) && BDPT_LEAF_EARLY && !spec_trav(LM); }
-#ifndef BDPT_SPEC_TWO
-#define BDPT_SPEC_TWO 0   // up to two postponed leaves per lane: measured -6% (Lucy stand-in), -4% C5-shaped
-#endif
-#ifndef BDPT_SPEC_ANY
-#define BDPT_SPEC_ANY 1   // connection rays too (Lucy stand-in +0.6% over closest hit alone)
-#endif
-// The descent stops once fewer than BDPT_SPEC_MIN lanes still look for their first leaf (1: once
-// all have one); the others go on after the leaf tests. Measured on the Lucy stand-in: 1 630, 4 574,
-// 8 523, 16 491 Msamples/s (stragglers then descend alone); speculation in the LDS-resident tree
-// (BDPT_SPEC_LM1) with 8: CBgems m7 269 -> 201.
-#ifndef BDPT_SPEC_MIN
-#define BDPT_SPEC_MIN 1
-#endif
+// postponed leaf keeps descending while other lanes still look for theirs; leaves are tested once
+// every lane holds one (or is done). Where the nodes come from HBM (LM 0 / 2) the extra node steps
+// fill the lanes that would otherwise wait: Lucy stand-in 601 -> 631, C5-shaped 468 -> 485
+// Msamples/s; with the whole tree in LDS (LM 1) the longer steps cost more than the latency they
+// hide (CBgems m7 269 -> 247), so only LM 0 / 2. Variants measured and removed: two
+// postponed leaves per lane, stopping the descent once fewer than 4 / 8 / 16 lanes still look.
+BDPT_HD constexpr bool spec_trav(int LM) { return LM == 0 || LM == 2; }
 // active lanes of the wave for which the predicate holds (the host build runs one lane)
 BDPT_HD int wave_count(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -449,23 +410,8 @@ BDPT_HD int wave_count(bool p) {
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
 BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
-// 4-wide nodes with quantized child boxes (64 B instead of 128 B): the parent's fp32 origin and a
-// power-of-two step per axis, each child plane an 8-bit multiple of the step rounded outward, so a
-// decoded box contains the padded fp32 box (checked exactly when the host emits it). Half the
-// node bytes: twice the treelet in the same LDS, half the L2 / Infinity-Cache footprint.
-#ifndef BDPT_QNODE
-#define BDPT_QNODE 0
-#endif
-// 4-wide fp32 nodes: the slab planes as packed fmas (v_pk_fma_f32, two children per instruction)
-#ifndef BDPT_PK_SLAB
-#define BDPT_PK_SLAB 0
-#endif
-// LM 2 node fetches: wave-uniform LDS-only / HBM-only paths, mixed waves fetch both (node_step)
-#ifndef BDPT_NODE_SPLIT
-#define BDPT_NODE_SPLIT 1
-#endif
-BDPT_HD constexpr int node_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 8) : 4; }        // float4 per node (stride)
-BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? (BDPT_QNODE ? 4 : 7) : 4; }   // float4 a traversal reads
+BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
+BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
@@ -599,46 +545,6 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
 #endif
 }
 
-// A node from HBM as one asm block of global loads and its own wait (BDPT_NODE_SPLIT 2): nothing
-// is left in flight into the registers the LDS path's ds_reads write, so the compiler puts no
-// vmcnt wait (for these loads, or for unrelated scratch stores) in front of those ds_reads.
-template <int W>
-BDPT_HD void ld_node_glb(const float4* p, float4* v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const __attribute__((address_space(1))) float4* g = (const __attribute__((address_space(1))) float4*)p;
-  v4f t[7];
-  if (node_used_f4(W) == 7) {
-    asm volatile(
-        "global_load_dwordx4 %0, %7, off\n\t"
-        "global_load_dwordx4 %1, %7, off offset:16\n\t"
-        "global_load_dwordx4 %2, %7, off offset:32\n\t"
-        "global_load_dwordx4 %3, %7, off offset:48\n\t"
-        "global_load_dwordx4 %4, %7, off offset:64\n\t"
-        "global_load_dwordx4 %5, %7, off offset:80\n\t"
-        "global_load_dwordx4 %6, %7, off offset:96\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
-        : "v"(g)
-        );
-  } else {
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off\n\t"
-        "global_load_dwordx4 %1, %4, off offset:16\n\t"
-        "global_load_dwordx4 %2, %4, off offset:32\n\t"
-        "global_load_dwordx4 %3, %4, off offset:48\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
-        : "v"(g)
-        );
-  }
-#pragma unroll
-  for (int k = 0; k < node_used_f4(W); k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
-#else
-  for (int k = 0; k < node_used_f4(W); k++) v[k] = p[k];
-#endif
-}
-
 // One node of the descent: slab-test the children, continue with the nearest hit child, push the
 // other hit children (farther first, so they pop near-first); pop when none is hit.
 // Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
@@ -654,7 +560,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
     c.lnodes += W;
-  } else if (LM == 2 && BDPT_NODE_SPLIT) {
+  } else if (LM == 2) {
     // Treelet (LDS) and HBM lanes in one wave: a lane-divergent if / else over the same registers
     // runs the global loads, waits for them (the ds_reads would overwrite their registers), then
     // the ds_reads — HBM latency + LDS latency. Here only a wave whose lanes are all in the treelet
@@ -669,15 +575,10 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     if (all_lds) {
       ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
       c.lnodes += W;
-    } else if (BDPT_NODE_SPLIT == 2) {
-      ld_node_glb<W>(S.nodes + node_f4(W) * ref, v);
     } else {
 #pragma unroll
       for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
     }
-  } else if (LM == 2 && ref < S.ntop) {
-    ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
-    c.lnodes += W;
   } else {
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
@@ -705,97 +606,18 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     int r0, r1, r2, r3;
     float tn0, tn1, tn2, tn3;
     bool h0, h1, h2, h3;
-    if (BDPT_QNODE) {
-      // (o.x, o.y, o.z, biased exponents) | lo.x hi.x lo.y hi.y | lo.z hi.z ref0 ref1 | ref2 ref3 -,
-      // each plane word = four children's bytes. Plane p = o + q * 2^e, so its slab distance is
-      // fma(q, 2^e * inv, (o - ray.o) * inv): q * (2^e * inv) is exact, one rounding more than the
-      // fp32 box form, covered by the same 2^-16 padding the decoded box contains.
-      const float4 q0 = v[0], q1 = v[1 % NU], q2 = v[2 % NU], q3 = v[3 % NU];
-      const uint32_t ex = (uint32_t)__float_as_int(q0.w);
-      const float ax = __int_as_float((int)((ex & 0xffu) << 23)) * r.inv.x;
-      const float ay = __int_as_float((int)(((ex >> 8) & 0xffu) << 23)) * r.inv.y;
-      const float az = __int_as_float((int)(((ex >> 16) & 0xffu) << 23)) * r.inv.z;
-      const float bx = fmaf(q0.x, r.inv.x, -r.oi.x), by = fmaf(q0.y, r.inv.y, -r.oi.y), bz = fmaf(q0.z, r.inv.z, -r.oi.z);
-      const uint32_t wlx = (uint32_t)__float_as_int(q1.x), whx = (uint32_t)__float_as_int(q1.y);
-      const uint32_t wly = (uint32_t)__float_as_int(q1.z), why = (uint32_t)__float_as_int(q1.w);
-      const uint32_t wlz = (uint32_t)__float_as_int(q2.x), whz = (uint32_t)__float_as_int(q2.y);
-      r0 = __float_as_int(q2.z); r1 = __float_as_int(q2.w); r2 = __float_as_int(q3.x); r3 = __float_as_int(q3.y);
-      auto qslab = [&](int sh, float* tn) {   // child in byte sh/8 of every plane word
-        const float t0x = fmaf((float)((wlx >> sh) & 0xffu), ax, bx), t1x = fmaf((float)((whx >> sh) & 0xffu), ax, bx);
-        const float t0y = fmaf((float)((wly >> sh) & 0xffu), ay, by), t1y = fmaf((float)((why >> sh) & 0xffu), ay, by);
-        const float t0z = fmaf((float)((wlz >> sh) & 0xffu), az, bz), t1z = fmaf((float)((whz >> sh) & 0xffu), az, bz);
-        *tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-        return fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)) * 1.00000024f;
-      };
-      float tf;
-      tf = qslab(0, &tn0);
-      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
-      tf = qslab(8, &tn1);
-      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
-      tf = qslab(16, &tn2);
-      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
-      tf = qslab(24, &tn3);
-      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
-    } else {
     const float4 lx = v[0], hx = v[1], ly = v[2 % NU], hy = v[3 % NU];
     const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
     r0 = __float_as_int(e.x); r1 = __float_as_int(e.y); r2 = __float_as_int(e.z); r3 = __float_as_int(e.w);
-#if defined(__HIP_DEVICE_COMPILE__) && BDPT_PK_SLAB
-    if (true) {
-      // the 24 slab planes as 12 packed fmas (v_pk_fma_f32: two children per instruction; the same
-      // fused result per element as slab()), then slab()'s min / max per child
-      typedef float v2f __attribute__((ext_vector_type(2)));
-      const v2f ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
-      const v2f mx = {-r.oi.x, -r.oi.x}, my = {-r.oi.y, -r.oi.y}, mz = {-r.oi.z, -r.oi.z};
-      const v2f lx01 = __builtin_elementwise_fma((v2f){lx.x, lx.y}, ix, mx), lx23 = __builtin_elementwise_fma((v2f){lx.z, lx.w}, ix, mx);
-      const v2f hx01 = __builtin_elementwise_fma((v2f){hx.x, hx.y}, ix, mx), hx23 = __builtin_elementwise_fma((v2f){hx.z, hx.w}, ix, mx);
-      const v2f ly01 = __builtin_elementwise_fma((v2f){ly.x, ly.y}, iy, my), ly23 = __builtin_elementwise_fma((v2f){ly.z, ly.w}, iy, my);
-      const v2f hy01 = __builtin_elementwise_fma((v2f){hy.x, hy.y}, iy, my), hy23 = __builtin_elementwise_fma((v2f){hy.z, hy.w}, iy, my);
-      const v2f lz01 = __builtin_elementwise_fma((v2f){lz.x, lz.y}, iz, mz), lz23 = __builtin_elementwise_fma((v2f){lz.z, lz.w}, iz, mz);
-      const v2f hz01 = __builtin_elementwise_fma((v2f){hz.x, hz.y}, iz, mz), hz23 = __builtin_elementwise_fma((v2f){hz.z, hz.w}, iz, mz);
-      auto fin = [&](float t0x, float t1x, float t0y, float t1y, float t0z, float t1z, float* tn) {
-        *tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
-        return fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)) * 1.00000024f;
-      };
-      float tf;
-      tf = fin(lx01.x, hx01.x, ly01.x, hy01.x, lz01.x, hz01.x, &tn0);
-      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
-      tf = fin(lx01.y, hx01.y, ly01.y, hy01.y, lz01.y, hz01.y, &tn1);
-      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
-      tf = fin(lx23.x, hx23.x, ly23.x, hy23.x, lz23.x, hz23.x, &tn2);
-      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
-      tf = fin(lx23.y, hx23.y, ly23.y, hy23.y, lz23.y, hz23.y, &tn3);
-      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
-    } else
-#endif
-    {
-      float tf;
-      slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn0, &tf);
-      h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
-      slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn1, &tf);
-      h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
-      slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn2, &tf);
-      h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
-      slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
-      h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
-    }
-    }
-    if (ORD == 2) {
-      // continue with the nearest hit child, push the others in slot order (no sorting network)
-      const float k0 = h0 ? tn0 : INFINITY, k1 = h1 ? tn1 : INFINITY, k2 = h2 ? tn2 : INFINITY, k3 = h3 ? tn3 : INFINITY;
-      const float m01 = fminf(k0, k1), m23 = fminf(k2, k3);
-      const float mn = fminf(m01, m23);
-      if (!(mn < INFINITY)) {
-        int nx;
-        return stk.pop(nx) ? nx : kTravDone;
-      }
-      const int best = mn == k0 ? 0 : mn == k1 ? 1 : mn == k2 ? 2 : 3;
-      if (h3 && best != 3) stk.push(r3);
-      if (h2 && best != 2) stk.push(r2);
-      if (h1 && best != 1) stk.push(r1);
-      if (h0 && best != 0) stk.push(r0);
-      return best == 0 ? r0 : best == 1 ? r1 : best == 2 ? r2 : r3;
-    }
+    float tf;
+    slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn0, &tf);
+    h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
+    slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn1, &tf);
+    h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
+    slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn2, &tf);
+    h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
+    slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
+    h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
     if (ORD == 0) {
       // continue with the lowest hit slot, push the others
       int nx = kTravDone;
@@ -845,7 +667,6 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   int ref = S.root;
   c.closest++;
   int li = 0;
-#if BDPT_FLAT_PREFETCH
   if (LM == 3 && S.fn > 0) {
     // the flat list as one run of primitives, the next record's loads issued before this test
     float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
@@ -872,16 +693,11 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     if (h.prim >= 0) c.hits++;
     return h.prim >= 0;
   }
-#endif
   float4 a0, a1, a2;
-  auto fetch_leaf = [&](int lr) {   // leaf_early: first record of leaf lr
-    const int s3 = 3 * leaf_start(lr);
-    a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
-  };
   // the primitives of leaf lf, closest hit so far in h
   auto test_leaf = [&](int lf) {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
-    if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
+    if constexpr (leaf_prefetch(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
@@ -926,31 +742,15 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     // speculative while-while: a lane's first leaf is postponed and the lane goes on descending its
     // stack while other lanes still look for theirs; leaves are tested once every lane has one
     int pend = 0;
-#if BDPT_SPEC_TWO
-    int pend2 = 0;   // a second postponed leaf
-#endif
     for (;;) {
       while (ref >= 0) {
-        ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
+        ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-#if BDPT_SPEC_TWO
-        else if (ref < 0 && ref != kTravDone && pend2 == 0) {
-          pend2 = ref;
-          if (!stk.pop(ref)) ref = kTravDone;
-        }
-#endif
-        if (wave_count(pend == 0 && ref >= 0) < BDPT_SPEC_MIN) break;
+        if (wave_count(pend == 0 && ref >= 0) == 0) break;
       }
-#if BDPT_SPEC_TWO
-      if (pend2 != 0) {
-        const int lf = pend2;
-        pend2 = 0;
-        test_leaf(lf);
-      }
-#endif
       while (pend != 0) {
         test_leaf(pend);
         pend = 0;
@@ -962,21 +762,16 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       if (ref == kTravDone) break;
     }
   } else {
-  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-  for (;;) {
-    if (LM == 3) {
-      if (li >= S.nleaves) break;
-      ref = ld_lds_i(S.lleaves + li++);
+    for (;;) {
+      if (LM == 3) {
+        if (li >= S.nleaves) break;
+        ref = ld_lds_i(S.lleaves + li++);
+      }
+      while (ref >= 0) ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
+      if (ref == kTravDone) break;
+      test_leaf(ref);
+      if (LM != 3 && !stk.pop(ref)) break;
     }
-    while (ref >= 0) {
-      ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
-      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-    }
-    if (ref == kTravDone) break;
-    test_leaf(ref);
-    if (LM != 3 && !stk.pop(ref)) break;
-    if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
-  }
   }
   if (h.prim >= 0) c.hits++;
   return h.prim >= 0;
@@ -991,7 +786,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   int ref = S.root;
   c.shadow++;
   int li = 0;
-#if BDPT_FLAT_PREFETCH
   if (LM == 3 && S.fn > 0) {
     float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
     for (int pi = 0; pi < S.fn; pi++) {
@@ -1011,16 +805,11 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     }
     return false;
   }
-#endif
   float4 a0, a1, a2;
-  auto fetch_leaf = [&](int lr) {   // leaf_early: first record of leaf lr
-    const int s3 = 3 * leaf_start(lr);
-    a0 = ld_geom<LM>(S, s3); a1 = ld_geom<LM>(S, s3 + 1); a2 = ld_geom<LM>(S, s3 + 2);
-  };
   // true if a primitive of leaf lf is hit on [tmin, tmax]
   auto test_leaf = [&](int lf) -> bool {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
-    if constexpr (leaf_prefetch(LM) && !leaf_early(LM)) {
+    if constexpr (leaf_prefetch(LM)) {
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
@@ -1051,34 +840,18 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     }
     return false;
   };
-  if constexpr (spec_trav(LM) && BDPT_SPEC_ANY) {
+  if constexpr (spec_trav(LM)) {
     // speculative while-while, as in trace_closest
     int pend = 0;
-#if BDPT_SPEC_TWO
-    int pend2 = 0;   // a second postponed leaf
-#endif
     for (;;) {
       while (ref >= 0) {
-        ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
+        ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-#if BDPT_SPEC_TWO
-        else if (ref < 0 && ref != kTravDone && pend2 == 0) {
-          pend2 = ref;
-          if (!stk.pop(ref)) ref = kTravDone;
-        }
-#endif
-        if (wave_count(pend == 0 && ref >= 0) < BDPT_SPEC_MIN) break;
+        if (wave_count(pend == 0 && ref >= 0) == 0) break;
       }
-#if BDPT_SPEC_TWO
-      if (pend2 != 0) {
-        const int lf = pend2;
-        pend2 = 0;
-        if (test_leaf(lf)) return true;
-      }
-#endif
       while (pend != 0) {
         if (test_leaf(pend)) return true;
         pend = 0;
@@ -1090,21 +863,16 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       if (ref == kTravDone) return false;
     }
   } else {
-  if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-  for (;;) {
-    if (LM == 3) {
-      if (li >= S.nleaves) return false;
-      ref = ld_lds_i(S.lleaves + li++);
+    for (;;) {
+      if (LM == 3) {
+        if (li >= S.nleaves) return false;
+        ref = ld_lds_i(S.lleaves + li++);
+      }
+      while (ref >= 0) ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
+      if (ref == kTravDone) return false;
+      if (test_leaf(ref)) return true;
+      if (LM != 3 && !stk.pop(ref)) return false;
     }
-    while (ref >= 0) {
-      ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
-      if (leaf_early(LM) && ref < 0 && ref != kTravDone) fetch_leaf(ref);
-    }
-    if (ref == kTravDone) return false;
-    if (test_leaf(ref)) return true;
-    if (LM != 3 && !stk.pop(ref)) return false;
-    if (leaf_early(LM) && ref < 0) fetch_leaf(ref);
-  }
   }
 }
 
@@ -1114,7 +882,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
 template <int LM, int K>
 BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
                                              int& ref, TravStack<K>& stk, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, BDPT_CLOSEST_ORD>(S, r, ref, tmin, h.t, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
   if (ref == kTravDone) return true;
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -1143,7 +911,7 @@ BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float
 template <int LM, int K>
 BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
                                          int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, BDPT_ANY_ORD>(S, r, ref, tmin, tmax, stk, c);
+  while (ref >= 0) ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
   if (ref == kTravDone) { *hit = false; return true; }
   const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
   for (int k = 0; k < cnt; k++) {
@@ -1532,89 +1300,6 @@ BDPT_HD float step_gx(f3 cur_pos, f3 cur_n, bool cur_env, f3 oth_pos, f3 oth_zh,
 }
 BDPT_HD bool is_env(const Vtx& v) { return v.mat == MAT_ENV_V; }
 
-// The walk computes each vertex's MIS constants when the vertex is created (prepare_sample,
-// BDPT_FUSED_CONSTANTS); the two passes below are the reference-shaped form of the same values,
-// kept for BDPT_FUSED_CONSTANTS=0 A/B builds.
-#ifndef BDPT_FUSED_CONSTANTS
-#define BDPT_FUSED_CONSTANTS 1
-#endif
-// Per-subpath MIS constants (see Vtx). EXT: the scene has an environment light or the walks use
-// Russian roulette (q = Vtx::gp on entry); EXT = false compiles to the reference-only path.
-template <int MAXV, bool EXT = false>
-BDPT_HD void eye_constants(const SceneView& S, Paths<MAXV>& P) {
-  const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
-  int nh = P.nE - 2;
-  for (int k = 0; k < nh; k++) {   // vertex E[k+2]
-    Vtx& v = P.E[k];
-    const bool venv = EXT && is_env(v);
-    f3 prevp = k == 0 ? cam : P.E[k - 1].pos;
-    const bool conn = !venv && S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(prevp, v.pos)), v.zh) >= 0 &&
-                      nonzero3(v.alpha);
-    v.cq = conn ? (EXT ? v.gp : 1.0f) : 0.0f;
-    if (k == 0) {
-      v.fwd = 1.0f * 1.0f;
-    } else {
-      const Vtx& nx = P.E[k - 1];
-      f3 dw;
-      float g2 = EXT ? step_gx(v.pos, v.n, venv, nx.pos, nx.zh, false, &dw) : step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
-      float p = pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * (EXT ? nx.gp : 1.0f);
-      v.fwd = p * g2;
-    }
-  }
-  float G = 0.0f;
-  for (int k = 0; k < nh; k++) {   // vertex E[k+2]
-    Vtx& v = P.E[k];
-    v.gp = G;
-    if (k + 1 < nh) {
-      const Vtx& pv = P.E[k + 1];
-      if (EXT && is_env(pv)) {
-        G = 0.0f;   // an escaped vertex ends the path; the j = 0 weight recomputes this step
-      } else {
-        f3 dw;
-        float g = step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-        float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * (EXT ? pv.gp : 1.0f);
-        G = mis_horner((p * g) / v.fwd, !((P.dE >> (k + 1)) & 3u), G);
-      }
-    }
-  }
-}
-
-template <int MAXV, bool EXT = false>
-BDPT_HD void light_constants(const SceneView& S, Paths<MAXV>& P, float l1_p) {
-  int nv = P.nL - 1;   // L[1..nL-1]
-  const bool l1env = EXT && is_env(P.L[0]);
-  for (int k = 0; k < nv; k++) {   // vertex L[k+1]
-    Vtx& v = P.L[k];
-    if (k == 0) {
-      v.fwd = l1_p;
-      v.cq = 0.0f;
-      continue;
-    }
-    const Vtx& nx = P.L[k - 1];
-    const bool conn = S.mats[v.mat].type == MAT_DIFFUSE && lz(normalize(sub(nx.pos, v.pos)), v.zh) >= 0 &&
-                      nonzero3(v.alpha);
-    v.cq = conn ? (EXT ? v.gp : 1.0f) : 0.0f;
-    f3 dw;
-    float g2 = EXT ? step_gx(v.pos, v.n, false, nx.pos, nx.zh, k == 1 && l1env, &dw)
-                   : step_g(v.pos, v.n, nx.pos, nx.zh, &dw);
-    float p = (k == 1) ? P.l1_dir_pdf : pdf_b(S.mats[nx.mat], nx.n, nx.zh, dw) * (EXT ? nx.gp : 1.0f);
-    v.fwd = p * g2;
-  }
-  float G = 0.0f;
-  for (int k = 0; k < nv; k++) {   // vertex L[k+1]
-    Vtx& v = P.L[k];
-    v.gp = G;
-    if (k + 1 < nv) {
-      const Vtx& pv = P.L[k + 1];
-      f3 dw;
-      float g = EXT ? step_gx(v.pos, v.n, k == 0 && l1env, pv.pos, pv.zh, false, &dw)
-                    : step_g(v.pos, v.n, pv.pos, pv.zh, &dw);
-      float p = pdf_b(S.mats[pv.mat], pv.n, pv.zh, dw) * (EXT ? pv.gp : 1.0f);
-      G = mis_horner((p * g) / v.fwd, !((P.dL >> k) & 3u), G);
-    }
-  }
-}
-
 // AreaLight/PointLight BDPT methods (light.cpp:115-153, 219-284).
 BDPT_HD bool light_contains(const DLight& l, f3 p) {
   f3 lp = mk3(l.pos[0], l.pos[1], l.pos[2]);
@@ -1744,9 +1429,6 @@ BDPT_HD EyeSample camera_sample(const DCam& c, int W, int H, f3 p) {
 template <bool EXT = false, class PA>
 BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const Vtx* lv, int i, int j,
                          const LightSample& ls, const EyeSample& es, int eye_light, f3 dc, float dist) {
-#ifdef BDPT_EXP_NOMIS
-  return 0.5f;
-#endif
   float ge = 0.0f, gl = 0.0f;
   if (i >= 2) {
     const Vtx& cur = *ev;
@@ -1824,16 +1506,6 @@ struct PathsInRegs {
 // eye walk ends starts its light walk in the next iteration, so a wave iterates
 // max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
 // sample + walk: 1) make the interleaving invisible in the results.
-// Drop the RNG's cached Philox block before each walk traversal: 4 fewer registers live across it,
-// at most one extra Philox evaluation per bounce. Measured slower (fewer spills, more VALU): off.
-#ifndef BDPT_RNG_DROP
-#define BDPT_RNG_DROP 0   // measured: off is +1% (Lucy stand-in 591 -> 598, CBspheres +1.3%)
-#endif
-// 0: light sample drawn before the walk and held in registers; 1: drawn when the eye walk ends;
-// 2: drawn before the walk, read back from the path store when the light walk starts
-#ifndef BDPT_LATE_LIGHT
-#define BDPT_LATE_LIGHT 2
-#endif
 template <int MAXV, int LM = 0, bool EXT = false>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
@@ -1922,7 +1594,6 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused walk)
     P.l1_dir_pdf = mis_dir;
   };
-#if BDPT_LATE_LIGHT != 1
   Rng gl0 = g;
   f3 lo, ld, ln, la1;
   float ldp;
@@ -1934,12 +1605,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   cnt.clk_light += __builtin_amdgcn_s_memtime() - tl0;
 #endif
   const uint32_t lpos = gl0.pos;
-#if BDPT_LATE_LIGHT == 2
   P.l1_d = ld;
   P.l1_pdf = ldp;
   l1env = false;   // re-read with the rest when the light walk starts
-#endif
-#endif
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
   f3 ro = cam;
   float rmin = S.cam.nclip, rmax = S.cam.fclip;
@@ -1951,18 +1619,13 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   int i = 2, count = 0;
   uint32_t dm = 0;
   bool light = false;
-#if BDPT_FUSED_CONSTANTS
   // the previous vertex's material / fwd / prefix / roulette probability (fused constants)
   int pv_mat = -1;
   float pv_fwd = 1.0f, pv_gp = 0.0f, pv_q = 1.0f;
-#endif
   for (;;) {
     Hit h;
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
-#endif
-#if BDPT_RNG_DROP
-    g.cur = 0xffffffffu;   // the Philox block cache is not kept across the traversal (recomputed)
 #endif
     bool end = !trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
@@ -1978,12 +1641,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.zh = v.n;
       v.mat = MAT_ENV_V;
       v.fwd = 1; v.gp = 1; v.cq = 0;
-#if BDPT_FUSED_CONSTANTS
       // eye_constants of an env vertex: g = 1 toward it, the previous vertex's BSDF density of rd
       // times its roulette probability; no prefix (the j = 0 weight recomputes this step)
       if (count > 0) v.fwd = pdf_b(S.mats[pv_mat], prev_n, zaxis(prev_n), rd) * pv_q * 1.0f;
       v.gp = 0.0f;
-#endif
       P.E[count++] = v;
     }
     if (!end) {
@@ -2002,7 +1663,6 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
       Vtx* slot = (light ? P.L + 1 : P.E) + count++;
       if (is_delta(M.type)) dm |= 1u << i;
-#if BDPT_FUSED_CONSTANTS
       // eye_constants / light_constants of this vertex at its creation. The previous vertex is the
       // one just below it on the same subpath (camera: no step; the light vertex L[1] for the
       // light's first hit) and is still in registers: position ro, normal prev_n (shading axis
@@ -2033,16 +1693,13 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp; pv_q = q;
       };
       if (!EXT) finish(1.0f);
-#endif
       *slot = v;
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
-#if BDPT_FUSED_CONSTANTS
         if (EXT) {
           finish(1.0f);
           slot->gp = v.gp; slot->cq = v.cq;
         }
-#endif
       } else {
         f3 wi;
         float pdf;
@@ -2054,12 +1711,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
           slot->gp = q;
           if (!(rng_next(g) < q)) end = true;
         }
-#if BDPT_FUSED_CONSTANTS
         if (EXT) {
           finish(q);
           slot->gp = v.gp; slot->cq = v.cq;
         }
-#endif
         ro = hit_p;
         rd = normalize(to_world(fr, wi));
         rmin = BDPT_EPS_F;
@@ -2081,14 +1736,6 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       P.nE = count + 2;
       P.dE = dm;
       light = true;
-#if BDPT_LATE_LIGHT == 1
-      {
-        f3 a1;
-        float pdf1;
-        sample_light(g, ro, rd, prev_n, a1, pdf1);
-        nalpha = next_alpha(a1, prev_n, rd, splat3(1.0f), pdf1);
-      }
-#elif BDPT_LATE_LIGHT == 2
       // the light sample drawn before the eye walk, read back from the path store (not held in
       // registers across the eye walk)
       rng_stream(g, 1);
@@ -2097,22 +1744,10 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       nalpha = next_alpha(P.L[0].alpha, prev_n, rd, splat3(1.0f), P.l1_pdf);
       mis_p = P.L[0].fwd;
       l1env = P.L[0].mat == (int)MAT_ENV_V;
-#else
-      rng_stream(g, 1);
-      g.pos = lpos;
-      ro = lo; rd = ld; prev_n = ln;
-      nalpha = next_alpha(la1, prev_n, rd, splat3(1.0f), ldp);
-#endif
       rmin = BDPT_EPS_F; rmax = INFINITY;
       i = 2; count = 0; dm = 0;
-#if BDPT_FUSED_CONSTANTS
       pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
-#endif
     }
-  }
-  if (!BDPT_FUSED_CONSTANTS) {
-    eye_constants<MAXV, EXT>(S, P);
-    light_constants<MAXV, EXT>(S, P, P.L[0].fwd);
   }
 }
 

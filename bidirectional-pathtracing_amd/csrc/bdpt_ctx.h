@@ -110,11 +110,8 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.env.cond = c->d_env ? c->d_env + hs.env_h : nullptr;
   S.env.pdf = c->d_env ? c->d_env + hs.env_h + np : nullptr;
   S.env.rgb = c->d_env ? c->d_env + hs.env_h + 2 * np : nullptr;
-#ifndef BDPT_ENV_GUIDE
-#define BDPT_ENV_GUIDE 1   // 0: plain binary searches (A/B)
-#endif
-  S.env.gmarg = c->d_env && BDPT_ENV_GUIDE ? (const int*)(c->d_env + hs.env_h + 5 * np) : nullptr;
-  S.env.gcond = c->d_env ? S.env.gmarg + hs.env_gm + 1 : nullptr;
+  S.env.gmarg = c->d_env ? (const int*)(c->d_env + hs.env_h + 5 * np) : nullptr;
+  S.env.gcond = S.env.gmarg ? S.env.gmarg + hs.env_gm + 1 : nullptr;
   S.env.gm = hs.env_gm;
   S.env.gc = hs.env_gc;
   S.env.cx = hs.env_c[0]; S.env.cy = hs.env_c[1]; S.env.cz = hs.env_c[2];

@@ -136,110 +136,6 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
   }
 }
 
-// Per-lane cache of one light-image target: splats to the cached pixel are summed in registers
-// and written once at the end of the kernel. A point light's t = 1, s = 1 connections all project
-// to one pixel, so every lane ends up caching it and those splats cost no global atomics at all.
-struct SplatCache {
-  int tgt = -1;
-  float x = 0, y = 0, z = 0;
-  __device__ void add(float* light, int t, float vx, float vy, float vz) {
-    if (tgt < 0) tgt = t;
-    if (t == tgt) {
-      x += vx; y += vy; z += vz;
-      return;
-    }
-    float* p = light + 3 * (size_t)t;
-    atomicAdd(p, vx);
-    atomicAdd(p + 1, vy);
-    atomicAdd(p + 2, vz);
-  }
-  // all 64 lanes: lanes caching the same pixel as the first pending lane are reduced first
-  __device__ void flush(float* light, int lane) {
-    bool on = tgt >= 0;
-#pragma unroll 1
-    for (int round = 0; round < 4; round++) {
-      const unsigned long long m = __ballot(on);
-      if (m == 0) return;
-      const int lead = __builtin_ctzll(m);
-      const int t0 = __shfl(tgt, lead, 64);
-      const bool same = on && tgt == t0;
-      if (__popcll(__ballot(same)) < 2) break;
-      const float sx = wave_sumf(same ? x : 0.0f), sy = wave_sumf(same ? y : 0.0f), sz = wave_sumf(same ? z : 0.0f);
-      if (lane == lead) {
-        float* p = light + 3 * (size_t)t0;
-        atomicAdd(p, sx);
-        atomicAdd(p + 1, sy);
-        atomicAdd(p + 2, sz);
-      }
-      on = on && !same;
-    }
-    if (on) {
-      float* p = light + 3 * (size_t)tgt;
-      atomicAdd(p, x);
-      atomicAdd(p + 1, y);
-      atomicAdd(p + 2, z);
-    }
-  }
-};
-
-// Resolves queued connection rays [head, tail) with lane refill: every lane takes an entry, and a
-// lane whose ray is done takes the next pending one (resumable any_step, bdpt_core.h), so the
-// wave's lanes stay busy until the queue runs dry instead of waiting for the slowest of 64 rays.
-#ifndef BDPT_FLUSH_REFILL
-#define BDPT_FLUSH_REFILL 0   // 1: drain the whole ring (64..127 rays) with lane refill; measured -0.5% Lucy, -6% CBspheres
-#endif
-template <int LM>
-__device__ __forceinline__ void flush_refill(const SceneView& S, WaveQ& q, int head, int tail, int lane, float* light,
-                                             Counters& cnt, SplatCache& sc) {
-  int next = head;   // wave-uniform
-  bool active = false;
-  int k = 0, ref = 0;
-  f3 o = splat3(0), d = splat3(0);
-  float tmax = 0;
-  RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
-  int stack_mem[BDPT_STACK];
-  TravStack<BDPT_CONN_STACK> stk(stack_mem);
-  for (;;) {
-    const unsigned long long idle = __ballot(!active);
-    const int take = min(__popcll(idle), tail - next);
-    if (!active) {
-      const int rank = lanes_below(idle);
-      if (rank < take) {
-        k = (next + rank) & (QCAP - 1);
-        o = mk3(q.ox[k], q.oy[k], q.oz[k]);
-        d = mk3(q.dx[k], q.dy[k], q.dz[k]);
-        tmax = q.tmax[k];
-        r = make_rayinv(o, d);
-        ref = S.root;
-        stk.clear();
-        cnt.shadow++;
-        active = true;
-      }
-    }
-    next += take;
-    if (__ballot(active) == 0) break;
-    for (;;) {
-      bool hit = false;
-      if (active && any_step<LM, BDPT_CONN_STACK>(S, r, o, d, BDPT_EPS_F, tmax, ref, stk, &hit, cnt)) {
-        active = false;
-        if (!hit) {
-          const int tgt = q.tgt[k];
-          if (tgt < 0) {
-            const int ow = ~tgt;
-            atomicAdd(&q.acc[0][ow], q.vx[k]);
-            atomicAdd(&q.acc[1][ow], q.vy[k]);
-            atomicAdd(&q.acc[2][ow], q.vz[k]);
-          } else {
-            sc.add(light, tgt, q.vx[k], q.vy[k], q.vz[k]);
-          }
-        }
-      }
-      const int na = __popcll(__ballot(active));
-      if (na == 0 || (na <= 56 && next < tail)) break;
-    }
-  }
-}
-
 // k_bdpt_sample: each lane owns one pixel and a chunk of its samples. Per sample the lane builds
 // both subpaths (random walks, closest-hit traversal) and then enumerates its (i, j) connections
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
@@ -262,22 +158,11 @@ constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
 #endif
 template <int MAXV>
 constexpr bool conn_compact() { return BDPT_CONN_COMPACT == 1 || (BDPT_CONN_COMPACT == 2 && MAXV >= 8); }
-// Connection loop order: 0 = the reference's (i outer, j inner), vertices reloaded per pair;
-// 1 = i outer with E[i] held across j; 2 = j outer with L[j] held across i.
-#ifndef BDPT_CONN_ORDER
-#define BDPT_CONN_ORDER 0
-#endif
 // Materials and lights copied to LDS (static arrays) when they fit: per-lane material / light
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
-#ifndef BDPT_MATS_LDS
-#define BDPT_MATS_LDS 1   // measured: C2 +3%, Lucy stand-in +1%, CBgems +1%
-#endif
+// (measured: C2 +3%, Lucy stand-in +1%, CBgems +1%)
 constexpr int kLdsMats = 48, kLdsLights = 8;
-#if BDPT_MATS_LDS
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
-#else
-constexpr size_t kStaticLds = 0;
-#endif
 
 #ifdef BDPT_PHASE_PROF
 #define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
@@ -308,7 +193,6 @@ __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DM
     kp.S.lnodes = sc;
     kp.S.lgeom = sc + nn;
   }
-#if BDPT_MATS_LDS
   if (kp.nmat <= kLdsMats && kp.S.nlights <= kLdsLights) {
     for (int k = threadIdx.x; k < kp.nmat; k += blockDim.x) s_mats[k] = kp.S.mats[k];
     for (int k = threadIdx.x; k < kp.S.nlights; k += blockDim.x) s_lights[k] = kp.S.lights[k];
@@ -316,7 +200,6 @@ __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DM
     kp.S.mats = s_mats;
     kp.S.lights = s_lights;
   }
-#endif
 }
 
 // Persistent waves: each wave takes work items (8x8 pixel block, chunk of spl samples) from a
@@ -385,18 +268,10 @@ __device__ __forceinline__ bool next_item(const KParams& kp, int lane, int grp, 
   return true;
 }
 
-// Per-wave connection state of one work item: the direct (s = 0) eye contributions and the
-// wave-uniform ring indices (the eye accumulators live in the ring's LDS). BDPT_DIRECT_LDS: the
-// direct contributions go to the LDS accumulators too.
-#ifndef BDPT_DIRECT_LDS
-#define BDPT_DIRECT_LDS 1
-#endif
+// Per-wave connection state of one work item: the wave-uniform ring indices (the eye accumulators,
+// direct s = 0 contributions included, live in the ring's LDS).
 struct ConnState {
-  float dxs = 0, dys = 0, dzs = 0;
   int head = 0, tail = 0;
-#if BDPT_FLUSH_REFILL
-  SplatCache sc;   // flush_refill's per-lane light-image target, written out at the item's end
-#endif
 #ifdef BDPT_PHASE_PROF
   unsigned long long ph_gen = 0, ph_flush = 0;
 #endif
@@ -425,17 +300,11 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
     if (active) {
       kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre, EXT && STATS ? &cnt : nullptr);
       if (kind == CONN_DIRECT) {
-#if BDPT_DIRECT_LDS
         // straight into this lane's accumulator in the wave's LDS (only this wave writes it, and
         // not while a flush runs): no registers held across the walks
         q.acc[0][lane] += cn.val.x * inv;
         q.acc[1][lane] += cn.val.y * inv;
         q.acc[2][lane] += cn.val.z * inv;
-#else
-        cs.dxs += cn.val.x * inv;
-        cs.dys += cn.val.y * inv;
-        cs.dzs += cn.val.z * inv;
-#endif
       }
     }
     const bool push = kind == CONN_RAY;
@@ -456,16 +325,9 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
       PH_STAMP(tp0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-#if BDPT_FLUSH_REFILL
-      // every queued ray (64..127), idle lanes refilled from the backlog
-      flush_refill<LM>(kp.S, q, cs.head, cs.tail, lane, kp.light, cnt, cs.sc);
-      __builtin_amdgcn_wave_barrier();
-      cs.head = cs.tail;
-#else
       flush_queue<LM>(kp.S, q, cs.head, 64, lane, kp.light, cnt);
       __builtin_amdgcn_wave_barrier();
       cs.head += 64;
-#endif
       PH_STAMP(tp1);
 #ifdef BDPT_PHASE_PROF
       cs.ph_flush += tp1 - tp0;
@@ -496,23 +358,8 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
     }
   }
   } else {
-#if BDPT_CONN_ORDER == 1
-  // E[i] loaded once per i and kept in registers across the j loop
-  for (int i = 1; i < wE; i++) {
-    const Vtx ev = PP.e(i >= 2 ? i : 2);
-    for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL, i >= 2 ? &ev : nullptr);
-  }
-#elif BDPT_CONN_ORDER == 2
-  // j outer: L[j] loaded once per j and kept in registers across the i loop (the connections
-  // are order-free: per-connection RNG sub-streams, sums are fp32 atomics anyway)
-  for (int j = 0; j < wL; j++) {
-    const Vtx lv = PP.l(j >= 1 ? j : 1);
-    for (int i = 1; i < wE; i++) conn_step(i, j, i < nE && j < nL, nullptr, j >= 1 ? &lv : nullptr);
-  }
-#else
   for (int i = 1; i < wE; i++)
     for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
-#endif
   }
 #ifdef BDPT_PHASE_PROF
   cs.ph_gen += __builtin_amdgcn_s_memtime() - tg0;
@@ -526,19 +373,12 @@ __device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const I
   if (cs.tail > cs.head) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-#if BDPT_FLUSH_REFILL
-    flush_refill<LM>(kp.S, q, cs.head, cs.tail, lane, kp.light, cnt, cs.sc);
-#else
     flush_queue<LM>(kp.S, q, cs.head, cs.tail - cs.head, lane, kp.light, cnt);
-#endif
   }
-#if BDPT_FLUSH_REFILL
-  cs.sc.flush(kp.light, lane);
-#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (it.my_n > 0) {
-    float ax = q.acc[0][lane] + cs.dxs, ay = q.acc[1][lane] + cs.dys, az = q.acc[2][lane] + cs.dzs;
+    float ax = q.acc[0][lane], ay = q.acc[1][lane], az = q.acc[2][lane];
     float* e = kp.eye + 3 * ((size_t)it.x + (size_t)it.y * kp.sp.W);
     if (ax != 0) atomicAdd(e, ax);
     if (ay != 0) atomicAdd(e + 1, ay);
@@ -569,13 +409,8 @@ template <int MAXV, bool STATS, int LM, bool EXT>
 __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
   // One dynamic LDS array: [wave queues][optional scene / treelet copy]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#if BDPT_MATS_LDS
   __shared__ DMat s_mats[kLdsMats];
   __shared__ DLight s_lights[kLdsLights];
-#else
-  DMat* s_mats = nullptr;
-  DLight* s_lights = nullptr;
-#endif
   stage_scene<LM>(kp, smem, s_mats, s_lights);
   WaveQ* qs = (WaveQ*)smem;
   const int lane = threadIdx.x & 63;

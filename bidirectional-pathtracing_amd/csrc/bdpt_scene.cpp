@@ -231,41 +231,6 @@ float i2f(int v) {
   return f;
 }
 
-// A quantized 4-wide node (BDPT_QNODE; layout and decoding at node_step, bdpt_core.h): per axis
-// the origin o = the lowest child plane (fp32) and the smallest step 2^e with 255 * 2^e >= the
-// extent; each child plane becomes the multiple of the step rounded outward, so the decoded box
-// o + q * 2^e (exact in fp64) contains the padded fp32 box. Empty slots: ref kTravDone, q = 0.
-void emit_qnode(float* N, const float v[4][6], const int rf[4], int nch) {
-  std::memset(N, 0, 16 * sizeof(float));
-  uint32_t exps = 0;
-  uint32_t words[6] = {0, 0, 0, 0, 0, 0};   // lo.x hi.x lo.y hi.y lo.z hi.z, a byte per child
-  for (int a = 0; a < 3; a++) {
-    float lo = INFINITY, hi = -INFINITY;
-    for (int s = 0; s < nch; s++) {
-      lo = std::min(lo, v[s][a]);
-      hi = std::max(hi, v[s][3 + a]);
-    }
-    const double ext = (double)hi - (double)lo;
-    int e = -126;
-    while (e < 127 && 255.0 * std::ldexp(1.0, e) < ext) e++;
-    const double st = std::ldexp(1.0, e);
-    for (int s = 0; s < nch; s++) {
-      double ql = std::floor(((double)v[s][a] - lo) / st), qh = std::ceil(((double)v[s][3 + a] - lo) / st);
-      while (ql > 0 && (double)lo + ql * st > (double)v[s][a]) ql -= 1;
-      while (qh < 255 && (double)lo + qh * st < (double)v[s][3 + a]) qh += 1;
-      ql = std::max(0.0, std::min(255.0, ql));
-      qh = std::max(0.0, std::min(255.0, qh));
-      words[2 * a] |= (uint32_t)ql << (8 * s);
-      words[2 * a + 1] |= (uint32_t)qh << (8 * s);
-    }
-    N[a] = lo;
-    exps |= (uint32_t)(e + 127) << (8 * a);
-  }
-  std::memcpy(&N[3], &exps, 4);
-  std::memcpy(&N[4], words, sizeof words);
-  for (int s = 0; s < 4; s++) N[10 + s] = i2f(rf[s]);
-}
-
 }  // namespace
 
 int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err, bool pt) {
@@ -582,14 +547,6 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
         child_box(ch[1], N + 6);
         N[12] = i2f(ref_of(ch[0]));
         N[13] = i2f(ref_of(ch[1]));
-      } else if (BDPT_QNODE) {
-        float v[4][6] = {};
-        int rf[4] = {kTravDone, kTravDone, kTravDone, kTravDone};
-        for (int s = 0; s < (int)ch.size() && s < 4; s++) {
-          child_box(ch[s], v[s]);
-          rf[s] = ref_of(ch[s]);
-        }
-        emit_qnode(N, v, rf, std::min<int>(4, (int)ch.size()));
       } else {
         // SoA over the children: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] | refs[4] | pad;
         // an empty slot has ref kTravDone and a zero box (never read)

@@ -121,9 +121,9 @@ def test_flat_list_is_one_run_of_primitives(name, n, nsph):
 @pytest.mark.parametrize("scene,W,H,spp,M", [("scenes/CBbunny.dae", 64, 48, 2, 5),
                                              ("scenes/CBlucy_standin.dae", 48, 36, 2, 5)])
 def test_device_pipeline_bit_exact_mesh_trees(scene, W, H, spp, M):
-    """The 4-wide tree of a mesh scene (thousands of nodes, the quantized node format when
-    BDPT_QNODE is on; bvh.cpp:161-188 closest-hit semantics over a deep tree) vs mode 2: every
-    decoded child box must contain its primitives, or a hit goes missing and the images differ."""
+    """The 4-wide tree of a mesh scene (thousands of nodes; bvh.cpp:161-188 closest-hit semantics
+    over a deep tree) vs mode 2: every padded child box must contain its primitives, or a hit goes
+    missing and the images differ."""
     path = os.path.join(REPO, scene)
     if not os.path.exists(path):
         pytest.skip(f"{scene} not generated (tools/gen_standin.py, __graft_entry__.build)")
