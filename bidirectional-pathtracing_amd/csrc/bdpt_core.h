@@ -549,13 +549,11 @@ BDPT_HD void ld_node_lds(const float4* p, float4* v) {
 // other hit children (farther first, so they pop near-first); pop when none is hit.
 // Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
 // Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad
-// ORD: 1 = visit hit children near-first (closest-hit queries), 0 = in slot order (any-hit queries),
-// 2 = per lane: near-first iff `near` (trace_ray's mixed waves; slot order through the same sorting
-// network, keyed by slot index). A child is entered when its slab interval, clipped to [tmin, tmax],
-// is non-empty.
+// ORD: visit hit children near-first (closest-hit queries); any-hit queries take them in slot order.
+// A child is entered when its slab interval, clipped to [tmin, tmax], is non-empty.
 template <int K, int LM, int ORD = 1>
 BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
-                      Counters& c, bool near = true) {
+                      Counters& c) {
   constexpr int W = lm_width(LM), NU = node_used_f4(W);
   float4 v[NU];
   if (LM == 1) {   // all nodes in LDS: plain ds_reads the compiler schedules
@@ -595,7 +593,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     const bool hr = fmaxf(tnr, tmin) <= fminf(tfr, tmax);
     const int lref = __float_as_int(e.x), rref = __float_as_int(e.y);
     if (hl && hr) {
-      const bool lfirst = ORD == 0 || (ORD == 2 && !near) || tnl <= tnr;
+      const bool lfirst = ORD == 0 || tnl <= tnr;
       stk.push(lfirst ? rref : lref);
       return lfirst ? lref : rref;
     }
@@ -630,9 +628,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
       if (nx == kTravDone && !stk.pop(nx)) return kTravDone;
       return nx;
     }
-    // sort key: entry distance of a hit child (ORD 2 any-hit lanes: its slot), +inf for a miss or an
-    // empty slot
-    if (ORD == 2 && !near) { tn0 = 0.0f; tn1 = 1.0f; tn2 = 2.0f; tn3 = 3.0f; }
+    // sort key: entry distance of a hit child, +inf for a miss or an empty slot
     float k0 = h0 ? tn0 : INFINITY, k1 = h1 ? tn1 : INFINITY, k2 = h2 ? tn2 : INFINITY, k3 = h3 ? tn3 : INFINITY;
     // 5-comparator sorting network on (key, ref)
 #define BDPT_CSWAP(ka, ra, kb, rb)                          \
@@ -878,133 +874,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       if (LM != 3 && !stk.pop(ref)) return false;
     }
   }
-}
-
-// One query of either kind for waves that mix them (render_pixel_samples): closest hit in
-// [tmin, tmax] (ties in t to the larger DFS position, as trace_closest), or, with `any`, whether
-// anything is hit (as trace_any: slot-order children, done at the first hit). Same visits and hits
-// as the two dedicated loops.
-template <int LM = 0, int K = 0>
-BDPT_HD bool trace_ray(const SceneView& S, f3 o, f3 d, float tmin, float tmax, bool any, Hit& h, Counters& c) {
-  RayInv r = make_rayinv(o, d);
-  h.t = tmax;
-  h.prim = -1;
-  h.key = -1;
-  h.b1 = 0; h.b2 = 0;
-  int stack_mem[BDPT_STACK];
-  TravStack<K> stk(stack_mem);
-  int ref = S.root;
-  if (any) c.shadow++;
-  else c.closest++;
-  if (LM == 3 && S.fn > 0) {
-    // the flat list as one run of primitives, the next record's loads issued before this test
-    float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
-    for (int pi = 0; pi < S.fn; pi++) {
-      const float4 g0 = a0, g1 = a1, g2 = a2;
-      const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
-      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
-      float t, b1 = 0, b2 = 0;
-      bool ok;
-      int key;
-      if ((S.fsph >> pi) & 1u) {
-        c.sphs++;
-        ok = sph_test(g0, o, d, tmin, h.t, &t);
-        key = __float_as_int(g1.x);
-      } else {
-        c.tris++;
-        ok = tri_test(g0, g1, g2, o, d, tmin, h.t, &t, &b1, &b2);
-        key = __float_as_int(g2.y);
-      }
-      if (ok && (t < h.t || key > h.key)) {
-        h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
-        if (any) break;
-      }
-    }
-    if (h.prim >= 0 && !any) c.hits++;
-    return h.prim >= 0;
-  }
-  float4 a0, a1, a2;
-  // the primitives of leaf lf, closest hit so far in h; true once an any-hit query is answered
-  auto test_leaf = [&](int lf) -> bool {
-    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
-    if constexpr (leaf_prefetch(LM)) {
-      a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
-    }
-    for (int k = 0; k < cnt; k++) {
-      const int pi = st + k;
-      float t, b1 = 0, b2 = 0;
-      bool ok;
-      int key;
-      if constexpr (leaf_prefetch(LM)) {
-        const float4 g0 = a0, g1 = a1, g2 = a2;
-        const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
-        a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
-        if ((sm >> k) & 1) {
-          c.sphs++;
-          ok = sph_test(g0, o, d, tmin, h.t, &t);
-          key = __float_as_int(g1.x);
-        } else {
-          c.tris++;
-          ok = tri_test(g0, g1, g2, o, d, tmin, h.t, &t, &b1, &b2);
-          key = __float_as_int(g2.y);
-        }
-      } else {
-        if ((sm >> k) & 1) {
-          c.sphs++;
-          ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
-          key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
-        } else {
-          c.tris++;
-          const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
-          ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
-          key = __float_as_int(g2.y);
-        }
-      }
-      if (ok && (t < h.t || key > h.key)) {
-        h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
-        if (any) return true;
-      }
-    }
-    return false;
-  };
-  const bool near = !any;
-  if constexpr (spec_trav(LM)) {
-    int pend = 0;
-    for (;;) {
-      while (ref >= 0) {
-        ref = node_step<K, LM, 2>(S, r, ref, tmin, h.t, stk, c, near);
-        if (ref < 0 && ref != kTravDone && pend == 0) {
-          pend = ref;
-          if (!stk.pop(ref)) ref = kTravDone;
-        }
-        if (wave_count(pend == 0 && ref >= 0) == 0) break;
-      }
-      bool done = false;
-      while (pend != 0) {
-        if (test_leaf(pend)) { done = true; break; }
-        pend = 0;
-        if (ref < 0 && ref != kTravDone) {
-          pend = ref;
-          if (!stk.pop(ref)) ref = kTravDone;
-        }
-      }
-      if (done || ref == kTravDone) break;
-    }
-  } else {
-    int li = 0;
-    for (;;) {
-      if (LM == 3) {
-        if (li >= S.nleaves) break;
-        ref = ld_lds_i(S.lleaves + li++);
-      }
-      while (ref >= 0) ref = node_step<K, LM, 2>(S, r, ref, tmin, h.t, stk, c, near);
-      if (ref == kTravDone) break;
-      if (test_leaf(ref)) break;
-      if (LM != 3 && !stk.pop(ref)) break;
-    }
-  }
-  if (h.prim >= 0 && !any) c.hits++;
-  return h.prim >= 0;
 }
 
 // Resumable forms of the two queries for lane-refill loops: one call = descend to a leaf + test
@@ -2039,342 +1908,6 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
     }
   }
   return eye_sum;
-}
-
-// ================================================================================================
-// Connect-as-you-go: the sample loop of the megakernel. Per pixel-sample the light subpath is
-// walked first and stored (bidirection.cpp:484-487); the eye subpath is walked next (:476-481), and
-// each eye vertex E[i] is connected to every stored light vertex L[j] (:490-498) the moment it is
-// created, from registers: the eye subpath is never stored, only E[i-1]'s position, normal and MIS
-// constants are kept for the s = 0 weight. The camera connections (i = 1, light tracing) need only
-// the light subpath and run when it is complete. The RNG sub-streams (eye walk 0, light sample +
-// walk 1, fresh light sample of (i, 1): 2 + i) make the reordering invisible in the results, and the
-// eye-image contributions of a sample still come in the reference's (i, j) order.
-template <int MAXV>
-struct LightPath {
-  Vtx L[MAXV + 1];    // L[k] at index k - 1: L[1] = the light vertex, then the hits
-  int nL;             // subpath size including v0 (the reference's vector size)
-  uint32_t dL;        // bit k set <=> L[k] is_delta()
-  float l1_dir_pdf;   // L[1]'s direction density: the MIS density of the light's first step
-};
-
-// Path accessor of the connections of eye vertex E[i]: e() is only ever asked for E[i - 1] (the s = 0
-// weight's step below the emitter, make_conn / mis_weight), which the walk keeps in registers.
-template <int MAXV>
-struct EyeLightView {
-  const LightPath<MAXV>& LP;
-  const Vtx& eprev;
-  uint32_t dE, dL;
-  BDPT_HD EyeLightView(const LightPath<MAXV>& lp, const Vtx& ep, uint32_t de) : LP(lp), eprev(ep), dE(de), dL(lp.dL) {}
-  BDPT_HD Vtx e(int) const { return eprev; }
-  BDPT_HD Vtx l(int k) const { return LP.L[k - 1]; }
-};
-
-// One lane's walk (prepare_bidirectional_subpath, bidirection.cpp:20-102): the current ray and what
-// the next vertex's MIS constants need of the vertex below it.
-struct WalkLane {
-  f3 ro, rd, prev_n, nalpha;   // ray; normal of the vertex it leaves; throughput of the next vertex
-  float rmin, rmax;
-  int i, count;                // reference index of the next vertex; vertices created (hits)
-  uint32_t dm;                 // delta mask of this subpath
-  int pv_mat;                  // previous vertex: material, MIS denominator, prefix, roulette q
-  float pv_fwd, pv_gp, pv_q;
-  int phase;                   // 0 light walk, 1 eye walk, 2 no sample in progress
-};
-
-// the next vertex's throughput alpha = prev_alpha * |cos| * f / pdf (:60-62), formed when its ray is
-BDPT_HD f3 walk_next_alpha(f3 pa, f3 pn, f3 d, f3 f, float pdf) { return divs(mul(muls(pa, fabsf(dot(pn, d))), f), pdf); }
-
-// sample_light_ray (bidirection.cpp:105-118) with AreaLight / PointLight::sample_Le (light.cpp:115-123,
-// 219-232) or the environment light's, on stream 1: the light vertex L[1] and the
-// light walk's first ray.
-template <int MAXV, bool EXT>
-BDPT_HD void start_light_walk(const SceneView& S, LightPath<MAXV>& LP, WalkLane& w, Rng& g, Counters& cnt) {
-  rng_stream(g, 1);
-  int lid = (int)(rng_next(g) * (float)S.nlights);
-  if (lid >= S.nlights) lid = S.nlights - 1;
-  const DLight& L0 = S.lights[lid];
-  f3 lrad = mk3(L0.rad[0], L0.rad[1], L0.rad[2]);
-  f3 lo, ld, ln;
-  float lpp, ldp, mis_p, mis_dir;
-  bool l1env = false;
-  if (EXT && L0.type == LIGHT_ENV) {
-    // direction by sample_L's importance sampling, origin uniform on the disk of radius R facing -w,
-    // tangent to the scene's bounding sphere
-    f3 wv;
-    float pw;
-    lrad = env_sample_dir(S.env, g, &wv, &pw);
-    cnt.env_s++;
-    const float u1 = rng_next(g), u2 = rng_next(g);
-    const float r = S.env.rad * sqrtf(u1);
-    float c, sn;
-    cos_sin_2pi(u2, &c, &sn);
-    const Frame wf = make_frame(wv);
-    lo = add(add(add(mk3(S.env.cx, S.env.cy, S.env.cz), smul(S.env.rad, wv)), smul(r * c, wf.X)), smul(r * sn, wf.Y));
-    ld = neg(wv);
-    ln = ld;
-    lpp = 1.0f / L0.area;
-    ldp = pw;
-    mis_p = pw;
-    mis_dir = 1.0f / L0.area;
-    l1env = true;
-  } else if (L0.type == LIGHT_POINT) {
-    float z = rng_next(g) * 2 - 1;
-    float sinT = sqrtf(fmaxf(0.0f, 1.0f - z * z));
-    float u = rng_next(g);
-    float c, s;
-    cos_sin_2pi(u, &c, &s);
-    ld = mk3(c * sinT, s * sinT, z);
-    lo = mk3(L0.pos[0], L0.pos[1], L0.pos[2]);
-    lpp = 1;
-    ldp = 0.25f / BDPT_PI_F;
-    ln = ld;
-    mis_p = lpp;
-    mis_dir = ldp;
-  } else {
-    float sx, sy;
-    grid2d(g, &sx, &sy);
-    sx = sx - 0.5f;
-    sy = sy - 0.5f;
-    lo = add(add(mk3(L0.pos[0], L0.pos[1], L0.pos[2]), smul(sx, mk3(L0.dx[0], L0.dx[1], L0.dx[2]))),
-             smul(sy, mk3(L0.dy[0], L0.dy[1], L0.dy[2])));
-    f3 dl = cosine_hemi(g, &ldp);
-    Frame lf;
-    lf.X = mk3(L0.fx[0], L0.fx[1], L0.fx[2]);
-    lf.Y = mk3(L0.fy[0], L0.fy[1], L0.fy[2]);
-    lf.Z = mk3(L0.fz[0], L0.fz[1], L0.fz[2]);
-    ld = to_world(lf, dl);
-    lpp = 1.0f / L0.area;
-    ln = mk3(L0.dir[0], L0.dir[1], L0.dir[2]);
-    mis_p = lpp;
-    mis_dir = ldp;
-  }
-  lpp = lpp / (float)S.nlights;
-  mis_p = mis_p / (float)S.nlights;
-  const f3 alpha1 = divs(lrad, lpp);
-  Vtx& v1 = LP.L[0];
-  v1.pos = lo;
-  v1.n = ln;
-  v1.zh = l1env ? ln : zaxis(ln);
-  v1.alpha = alpha1;
-  v1.mat = l1env ? (int)MAT_ENV_V : -1;
-  v1.gp = 0; v1.cq = 0;
-  v1.fwd = mis_p;   // L[1]'s MIS point density
-  LP.l1_dir_pdf = mis_dir;
-  w.ro = lo; w.rd = ld; w.prev_n = ln;
-  w.nalpha = walk_next_alpha(alpha1, ln, ld, splat3(1.0f), ldp);
-  w.rmin = BDPT_EPS_F; w.rmax = INFINITY;
-  w.i = 2; w.count = 0; w.dm = 0;
-  w.pv_mat = -1; w.pv_fwd = mis_p; w.pv_gp = 0.0f; w.pv_q = 1.0f;
-  w.phase = 0;
-}
-
-// raytrace_pixel's jittered camera ray (bidirection.cpp:515-524) on stream 0, which the eye walk
-// continues: E[1] = {cam, n = d, alpha = 1, p = 1} (:476-481), first ray on [nClip, fClip].
-BDPT_HD void start_eye_walk(const SceneView& S, const SampleParams& sp, WalkLane& w, Rng& g, int x, int y) {
-  rng_stream(g, 0);
-  float px, py;
-  grid2d(g, &px, &py);
-  px = px + (float)x;
-  py = py + (float)y;
-  const float dx = px / (float)sp.W, dy = py / (float)sp.H;
-  const f3 rd = camera_dir(S.cam, dx, dy);
-  w.ro = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
-  w.rd = rd;
-  w.prev_n = rd;
-  w.nalpha = walk_next_alpha(divs(splat3(1.0f), 1.0f), rd, rd, splat3(1.0f), 1.0f);
-  w.rmin = S.cam.nclip; w.rmax = S.cam.fclip;
-  w.i = 2; w.count = 0; w.dm = 0;
-  w.pv_mat = -1; w.pv_fwd = 1.0f; w.pv_gp = 0.0f; w.pv_q = 1.0f;
-  w.phase = 1;
-}
-
-// One walk step after the closest-hit query of the lane's ray (h; `end` = it hit nothing): the hit
-// becomes the subpath's next vertex with its MIS constants (fwd, Horner prefix gp, connectability
-// cq), then sample_f (and roulette) give the next ray. A light vertex is stored in LP. An eye vertex
-// E[i] gets its s = 0 strategy (i, 0) here — the only one that needs E[i-1], so nothing of E[i-1]
-// outlives the step — whose value goes to wv.direct(); the vertex is returned in *ev with i in *ei
-// for the caller to connect to the light vertices. Returns true when the subpath has ended.
-template <int MAXV, int LM, bool EXT, class Wave>
-BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, LightPath<MAXV>& LP, WalkLane& w, Rng& g,
-                       Counters& cnt, Wave& wv, const Hit& h, bool end, bool* eye_new, Vtx* ev, int* ei) {
-  Vtx ep;   // E[i-1] (position, normal, fwd, prefix) for the (i, 0) strategy
-  Vtx* eprev = &ep;
-  const bool light = w.phase == 0;
-  *eye_new = false;
-  if (EXT && end && !light && S.env.light >= 0) {
-    // an escaped eye ray ends on the environment light: vertex at infinity in direction rd; g = 1
-    // toward it, the previous vertex's BSDF density of rd times its roulette probability; no
-    // prefix (the j = 0 weight recomputes this step)
-    Vtx v;
-    v.alpha = w.nalpha;
-    v.pos = w.ro;
-    v.n = neg(w.rd);
-    v.zh = v.n;
-    v.mat = MAT_ENV_V;
-    v.fwd = 1; v.gp = 0.0f; v.cq = 0;
-    if (w.count > 0) v.fwd = pdf_b(S.mats[w.pv_mat], w.prev_n, zaxis(w.prev_n), w.rd) * w.pv_q * 1.0f;
-    eprev->pos = w.ro; eprev->n = w.prev_n; eprev->fwd = w.pv_fwd; eprev->gp = w.pv_gp;
-    *ev = v;
-    *ei = w.i;
-    *eye_new = true;
-    w.count++;
-    Conn cn;
-    if (make_conn<EXT>(S, sp, EyeLightView<MAXV>(LP, ep, w.dm), g, w.i, 0, cn, ev, nullptr, &cnt) == CONN_DIRECT)
-      wv.direct(cn.val);
-  }
-  if (!end) {
-    f3 n;
-    int mat;
-    shade_hit<LM>(S, h, w.ro, w.rd, &n, &mat);
-    const DMat M = S.mats[mat];
-    const Frame fr = make_frame(n);
-    const f3 hit_p = add(w.ro, muls(w.rd, h.t));
-    Vtx v;
-    v.alpha = w.nalpha;
-    v.pos = hit_p;
-    v.n = n;
-    v.zh = fr.Z;
-    v.mat = mat;
-    v.fwd = 1; v.gp = 0.0f; v.cq = 0;
-    const int slot = w.count++;
-    if (is_delta(M.type)) w.dm |= 1u << w.i;
-    // The MIS constants of this vertex at its creation. The previous vertex is the one just below
-    // it on the same subpath (camera: no step; the light vertex L[1] for the light's first hit) and
-    // is still in registers: position ro, normal prev_n (shading axis normalize(prev_n), as
-    // make_frame / zaxis compute it; an environment L[1] keeps n itself), material, fwd, prefix,
-    // roulette probability. The prefix and the connectability need this vertex's own roulette
-    // probability, known after its sample_f below (EXT), so they are finished there:
-    // gp = horner(((pp * q) * g) / fwd_prev, t, gp_prev), cq = conn ? q : 0.
-    const bool conn = M.type == MAT_DIFFUSE && lz(normalize(sub(w.ro, v.pos)), v.zh) >= 0 && nonzero3(v.alpha);
-    const bool first_eye = !light && w.count == 1;
-    const bool first_light = light && w.count == 1;
-    float gp_pp = 0.0f, gp_g = 0.0f;
-    if (first_eye) {
-      v.fwd = 1.0f * 1.0f;
-    } else {
-      const bool nx_env = EXT && first_light && LP.L[0].mat == (int)MAT_ENV_V;
-      const f3 nx_zh = nx_env ? w.prev_n : zaxis(w.prev_n);
-      f3 dw;
-      const float g2 = EXT ? step_gx(v.pos, v.n, false, w.ro, nx_zh, nx_env, &dw) : step_g(v.pos, v.n, w.ro, nx_zh, &dw);
-      const float p = first_light ? LP.l1_dir_pdf : pdf_b(S.mats[w.pv_mat], w.prev_n, nx_zh, dw) * (EXT ? w.pv_q : 1.0f);
-      v.fwd = p * g2;
-      gp_g = EXT ? step_gx(w.ro, w.prev_n, nx_env, v.pos, v.zh, false, &dw) : step_g(w.ro, w.prev_n, v.pos, v.zh, &dw);
-      gp_pp = pdf_b(M, v.n, v.zh, dw);
-    }
-    if (!light) { eprev->pos = w.ro; eprev->n = w.prev_n; eprev->fwd = w.pv_fwd; eprev->gp = w.pv_gp; }
-    const bool gp_t = !((w.dm >> (w.i - 2)) & 3u);
-    float q = 1.0f;   // this vertex's roulette probability (1 without roulette)
-    f3 fv = splat3(0.0f), wi = splat3(0.0f);
-    float pdf = 1.0f;
-    if (w.i >= sp.max_depth + 1 || w.count >= MAXV) {
-      end = true;
-    } else {
-      fv = sample_f(M, g, to_local(fr, neg(w.rd)), &wi, &pdf);
-      if (EXT && sp.rr && w.i > BDPT_RR_MIN) {
-        // p_keep = min(1, |f| / pdf), PathVertex.q, then coin_flip(p_keep) (bidirection.cpp:87-93)
-        q = pdf > 0.0f ? fminf(1.0f, norm(fv) / pdf) : 0.0f;
-        if (!(rng_next(g) < q)) end = true;
-      }
-    }
-    v.cq = conn ? (EXT ? q : 1.0f) : 0.0f;
-    v.gp = first_eye ? 0.0f : mis_horner(((EXT ? gp_pp * q : gp_pp) * gp_g) / w.pv_fwd, gp_t, w.pv_gp);
-    w.pv_mat = v.mat; w.pv_fwd = v.fwd; w.pv_gp = v.gp; w.pv_q = q;
-    if (light) {
-      LP.L[1 + slot] = v;
-    } else {
-      *ev = v;
-      *ei = w.i;
-      *eye_new = true;
-      Conn cn;   // (i, 0): emission at E[i] (:307-328); draws no random numbers
-      if (make_conn<EXT>(S, sp, EyeLightView<MAXV>(LP, ep, w.dm), g, w.i, 0, cn, &v, nullptr, &cnt) == CONN_DIRECT)
-        wv.direct(cn.val);
-    }
-    if (!end) {
-      w.ro = hit_p;
-      w.rd = normalize(to_world(fr, wi));
-      w.rmin = BDPT_EPS_F;
-      w.rmax = INFINITY;
-      w.prev_n = n;
-      w.nalpha = walk_next_alpha(v.alpha, n, w.rd, fv, pdf * q);
-      w.i++;
-    }
-  }
-  return end;
-}
-
-// The samples [s0, s0 + n) of pixel (x, y), connect-as-you-go, on one lane of a wave. Every
-// iteration each lane traces ONE ray through the same traversal call (trace_ray): the next
-// connection ray of its newest eye vertex (or, once its light subpath is complete, of light tracing
-// to the camera), any-hit; else its next walk ray, closest-hit. A lane whose sample ends starts its
-// next one at once; the wave iterates until all of its lanes are through. Wave policy:
-//   bool wany(bool)            — wave-wide any (identity on a one-lane host build);
-//   void direct(f3)            — an s = 0 value of this lane (any control flow);
-//   void deliver(bool, const Conn&) — called by every lane together after each trace: true when
-//                                this lane's connection ray was unoccluded (cn = its value, target);
-//   void sample_done()         — after the last connection of a lane's sample (any control flow).
-// Returns the samples rendered.
-template <int MAXV, int LM, bool EXT, class Wave>
-BDPT_HD int render_pixel_samples(const SceneView& S, const SampleParams& sp, LightPath<MAXV>& LP, Counters& cnt,
-                                 int x, int y, uint32_t s0, int n, Wave& wv) {
-  WalkLane w;
-  w.phase = 2;
-  Rng g;
-  int t = 0;
-  Vtx ev;                     // the eye vertex being connected (ci >= 2)
-  int ci = 0, cj = 0, ce = 0;   // pending connections (ci, j) for j in [cj, ce)
-  bool tail = false;            // the sample's eye walk has ended; its last connections are pending
-  for (;;) {
-    // this lane's next connection that needs a ray: (ci, cj), (ci, cj + 1), ... (:385-455)
-    Conn cn;
-    bool conn = false;
-    while (cj < ce) {
-      Rng gc = g;
-      // w.dm: E[i]'s delta mask (the walk does not move on before E[i]'s connections are done)
-      const int kind = make_conn<EXT>(S, sp, EyeLightView<MAXV>(LP, ev, w.dm), gc, ci, cj, cn, ci >= 2 ? &ev : nullptr,
-                                      nullptr, &cnt);
-      cj++;
-      if (kind == CONN_RAY) { conn = true; break; }
-    }
-    if (tail && !conn) {
-      tail = false;
-      wv.sample_done();
-    }
-    if (!conn && w.phase == 2 && t < n) {   // the next sample (the light subpath is free again)
-      rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), s0 + (uint32_t)t);
-      start_light_walk<MAXV, EXT>(S, LP, w, g, cnt);
-    }
-    const bool walk = !conn && w.phase != 2;
-    if (!wv.wany(conn || walk)) break;
-    Hit h;
-    bool hit = false;
-    if (conn || walk)
-      hit = trace_ray<LM, BDPT_WALK_STACK>(S, conn ? cn.o : w.ro, conn ? cn.d : w.rd, conn ? BDPT_EPS_F : w.rmin,
-                                           conn ? cn.tmax : w.rmax, conn, h, cnt);
-    wv.deliver(conn && !hit, cn);
-    if (walk) {
-      const bool light = w.phase == 0;
-      bool eye_new = false;
-      int ei = 0;
-      const bool end = walk_step<MAXV, LM, EXT>(S, sp, LP, w, g, cnt, wv, h, !hit, &eye_new, &ev, &ei);
-      if (eye_new) {   // E[i] to every light vertex, (i, j) for j = 1 .. |L| - 1 (:490-498)
-        ci = ei; cj = 1; ce = LP.nL;
-      }
-      if (end) {
-        if (light) {   // light tracing: the camera to every light vertex, (1, j) (:360-383)
-          LP.nL = w.count + 2;
-          LP.dL = w.dm;
-          ci = 1; cj = 1; ce = LP.nL;
-          start_eye_walk(S, sp, w, g, x, y);
-        } else {
-          tail = true;
-          t++;
-          w.phase = 2;
-        }
-      }
-    }
-  }
-  return t;
 }
 
 // ================================================================================================

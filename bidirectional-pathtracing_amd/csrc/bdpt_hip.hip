@@ -27,11 +27,6 @@ using namespace bdpt;
 
 thread_local std::string bdpt::g_err;
 
-// 1: connect-as-you-go sample loop (render_pixel_samples); 0: both walks stored, then connected
-#ifndef BDPT_CAYG
-#define BDPT_CAYG 1
-#endif
-
 namespace {
 
 struct KParams {
@@ -80,16 +75,6 @@ struct WaveQ {
   int tgt[QCAP];            // >= 0: light-image pixel (t = 1 splat); < 0: ~owner lane (eye image)
   float acc[3][64];         // eye-image accumulators of the wave's 64 lanes
 };
-
-// The connect-as-you-go kernel keeps only the eye-image accumulators per wave in LDS (no ray ring).
-struct WaveAcc {
-  float acc[3][64];
-};
-#if BDPT_CAYG
-using WaveLds = WaveAcc;
-#else
-using WaveLds = WaveQ;
-#endif
 
 __device__ __forceinline__ float wave_sumf(float v) {
 #pragma unroll
@@ -191,7 +176,7 @@ constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLig
 template <int LM>
 __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DMat* s_mats, DLight* s_lights) {
   if (LM != 0) {
-    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveLds));
+    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
     const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
@@ -381,57 +366,6 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
 #endif
 }
 
-// The wave policy of render_pixel_samples (bdpt_core.h, connect-as-you-go): a lane's eye-image
-// values (s = 0, unoccluded connections) go to its accumulator in the wave's LDS (only this lane
-// writes it); light-tracing splats are fp32 atomics into the light frame, and splats aimed at the
-// most common target of the wave (a point light's own pixel takes every t = 1, s = 1 splat) are
-// summed across the wave first.
-struct LaneWave {
-  WaveAcc& q;
-  float* light;
-  int lane;
-  float inv;
-  __device__ bool wany(bool p) const { return __ballot(p) != 0; }
-  __device__ void sample_done() const {}
-  __device__ void direct(f3 v) {
-    q.acc[0][lane] += v.x * inv;
-    q.acc[1][lane] += v.y * inv;
-    q.acc[2][lane] += v.z * inv;
-  }
-  __device__ void deliver(bool vis, const Conn& cn) {
-    if (vis && cn.splat < 0) direct(cn.val);
-    const bool splat = vis && cn.splat >= 0;
-    const unsigned long long m = __ballot(splat);
-    if (m == 0) return;
-    const int tgt = splat ? cn.splat : -1;
-    const int lead = __builtin_ctzll(m);
-    const int t0 = __shfl(tgt, lead, 64);
-    const bool same = splat && tgt == t0;
-    const unsigned long long ms = __ballot(same);
-    if (__popcll(ms) > 1) {
-      const float sx = wave_sumf(same ? cn.val.x : 0.0f), sy = wave_sumf(same ? cn.val.y : 0.0f),
-                  sz = wave_sumf(same ? cn.val.z : 0.0f);
-      if (lane == lead) {
-        float* p = light + 3 * (size_t)t0;
-        atomicAdd(p, sx);
-        atomicAdd(p + 1, sy);
-        atomicAdd(p + 2, sz);
-      }
-    } else if (same) {
-      float* p = light + 3 * (size_t)t0;
-      atomicAdd(p, cn.val.x);
-      atomicAdd(p + 1, cn.val.y);
-      atomicAdd(p + 2, cn.val.z);
-    }
-    if (splat && !same) {
-      float* p = light + 3 * (size_t)tgt;
-      atomicAdd(p, cn.val.x);
-      atomicAdd(p + 1, cn.val.y);
-      atomicAdd(p + 2, cn.val.z);
-    }
-  }
-};
-
 // End of a work item: the queued rays are traced and every lane adds its eye-image sum once.
 template <int LM>
 __device__ __forceinline__ void finish_item(const KParams& kp, WaveQ& q, const Item& it, int lane, ConnState& cs,
@@ -478,31 +412,12 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
   __shared__ DMat s_mats[kLdsMats];
   __shared__ DLight s_lights[kLdsLights];
   stage_scene<LM>(kp, smem, s_mats, s_lights);
-  WaveLds* qs = (WaveLds*)smem;
+  WaveQ* qs = (WaveQ*)smem;
   const int lane = threadIdx.x & 63;
-  WaveLds& q = qs[threadIdx.x >> 6];
+  WaveQ& q = qs[threadIdx.x >> 6];
   Counters cnt = {0, 0, 0, 0, 0, 0};
   unsigned nsamp = 0;
   const float inv = 1.0f / (float)kp.sp.spp;
-#if BDPT_CAYG
-  LightPath<MAXV> LP;
-  const int grp = blockIdx.x & 7;
-  int cur = 0;   // wave-uniform: XCD groups exhausted so far
-  Item it;
-  while (next_item(kp, lane, grp, cur, it)) {
-    q.acc[0][lane] = 0;
-    q.acc[1][lane] = 0;
-    q.acc[2][lane] = 0;
-    LaneWave wv{q, kp.light, lane, inv};
-    nsamp += (unsigned)render_pixel_samples<MAXV, LM, EXT>(kp.S, kp.sp, LP, cnt, it.x, it.y, (uint32_t)it.s0, it.my_n, wv);
-    if (it.my_n > 0) {   // the lane's eye-image sum of the item, added once
-      float* e = kp.eye + 3 * ((size_t)it.x + (size_t)it.y * kp.sp.W);
-      if (q.acc[0][lane] != 0) atomicAdd(e, q.acc[0][lane]);
-      if (q.acc[1][lane] != 0) atomicAdd(e + 1, q.acc[1][lane]);
-      if (q.acc[2][lane] != 0) atomicAdd(e + 2, q.acc[2][lane]);
-    }
-  }
-#else
   Paths<MAXV> P;
 #ifdef BDPT_PHASE_PROF
   unsigned long long ph_prep = 0, ph_gen = 0, ph_flush = 0, tp0, tp1;
@@ -548,7 +463,6 @@ __global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KPar
     ph_flush += cs.ph_flush;
 #endif
   }
-#endif
 #ifdef BDPT_PHASE_PROF
   if (lane == 0) {
     atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
@@ -681,7 +595,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 #endif
 constexpr int kFlatMaxPrims = BDPT_FLAT_MAX_PRIMS;
 constexpr size_t kBlocksPerCu = 16 / kWavesPerBlock;
-constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveLds) - 256 - kStaticLds;
+constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256 - kStaticLds;
 
 // Persistent launch: as many blocks as are co-resident (occupancy query with this launch's LDS),
 // never more waves than work items.
@@ -699,7 +613,7 @@ int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
 
 // The LDS mode of a BDPT launch and the dynamic LDS it needs (wave queues + the scene copy).
 int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
-  const size_t q = kWavesPerBlock * sizeof(WaveLds);
+  const size_t q = kWavesPerBlock * sizeof(WaveQ);
   const size_t full = (c->hs.tree(lm_width(1)).nodes.size() + c->hs.geom.size()) * sizeof(float);
   const bool has_nodes = !c->hs.bvh2.nodes.empty();
   // LM 3's LDS: geometry, leaf list (padded to 16 B), shading records

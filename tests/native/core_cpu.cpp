@@ -18,30 +18,6 @@ struct HostSink {
   }
 };
 
-// The one-lane wave policy of render_pixel_samples (the kernel's connect-as-you-go loop): the
-// sample's eye value is summed in the reference's (i, j) order and added to the frame when the
-// sample ends, as render_sample's caller does.
-template <int LM>
-struct HostWave {
-  HostSink& sink;
-  int W;
-  float inv;
-  double* eye;
-  size_t k;
-  f3 sum = splat3(0);
-  bool wany(bool p) const { return p; }
-  void direct(f3 v) { sum = add(sum, v); }
-  void deliver(bool vis, const Conn& cn) {
-    if (!vis) return;
-    if (cn.splat >= 0) sink.splat(cn.splat % W, cn.splat / W, cn.val);
-    else sum = add(sum, cn.val);
-  }
-  void sample_done() {
-    eye[k] += (double)(sum.x * inv); eye[k + 1] += (double)(sum.y * inv); eye[k + 2] += (double)(sum.z * inv);
-    sum = splat3(0);
-  }
-};
-
 template <int MAXV, int LM, bool EXT>
 static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed, int s0, int count,
                const int* pixels, int npix, double* eye, double* light, double* stats, int rr) {
@@ -83,15 +59,18 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   std::vector<double> lb((size_t)W * H * 3, 0.0);
   HostSink sink{&lb, W};
   Counters cnt = {0, 0, 0, 0, 0, 0};
-  LightPath<MAXV>* LP = new LightPath<MAXV>();
+  Paths<MAXV>* P = new Paths<MAXV>();
   float inv = 1.0f / (float)spp;
   int total = pixels ? npix : W * H;
   for (int q = 0; q < total; q++) {
     int x = pixels ? pixels[2 * q] : q % W, y = pixels ? pixels[2 * q + 1] : q / W;
-    HostWave<LM> wv{sink, W, inv, eye, 3 * ((size_t)x + (size_t)y * W)};
-    render_pixel_samples<MAXV, LM, EXT>(S, sp, *LP, cnt, x, y, (uint32_t)s0, count, wv);
+    for (int s = s0; s < s0 + count; s++) {
+      f3 v = render_sample<MAXV, LM, EXT>(S, sp, *P, cnt, x, y, (uint32_t)s, sink);
+      size_t k = 3 * ((size_t)x + (size_t)y * W);
+      eye[k] += (double)(v.x * inv); eye[k + 1] += (double)(v.y * inv); eye[k + 2] += (double)(v.z * inv);
+    }
   }
-  delete LP;
+  delete P;
   for (size_t k = 0; k < lb.size(); k++) light[k] += lb[k];
   if (stats) {
     stats[0] = cnt.closest + cnt.shadow; stats[1] = cnt.closest; stats[2] = cnt.shadow;
