@@ -129,18 +129,22 @@ class Scene:
         e.rgb = self.envmap.ctypes.data_as(C.POINTER(C.c_float))
         self._env_desc = e
 
-    def load_camera(self, path: str) -> None:
+    def load_camera(self, path: str, focal_distance: float = 4.7, lens_radius: float = 0.0):
         """Application::load_camera -> Camera::load_settings (application.h:114-116, camera.cpp:172-186):
-        the -c camera-settings file through bdpt_camera_load_settings (w2c kept, as the reference
-        does not recompute it)."""
+        the -c camera-settings file through bdpt_camera_load_settings_lens (w2c kept, as the reference
+        does not recompute it). Returns the thin-lens settings the camera then holds: the file's
+        focalDistance and lensRadius, which replace the ones passed in (the config's -d / -b,
+        set_camera, raytraced_renderer.cpp:141-142) — give them to PathTracer(...)."""
         lib = load_library()
         cam = self.desc().camera
-        _check(lib.bdpt_camera_load_settings(os.fsencode(path), C.byref(cam)), lib)
+        fd, lr = C.c_double(focal_distance), C.c_double(lens_radius)
+        _check(lib.bdpt_camera_load_settings_lens(os.fsencode(path), C.byref(cam), C.byref(fd), C.byref(lr)), lib)
         c = dict(self.camera)
         c["pos"] = list(cam.pos)
         c["c2w_cols"] = [list(cam.c2w[3 * k:3 * k + 3]) for k in range(3)]
         c["hFov"], c["vFov"], c["nClip"], c["fClip"] = cam.hfov_deg, cam.vfov_deg, cam.nclip, cam.fclip
         self.camera = c
+        return fd.value, lr.value
 
     @property
     def nprim(self) -> int:
@@ -323,6 +327,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_dae_dump_json.argtypes = [C.c_void_p, C.c_char_p]
     lib.bdpt_dae_free.argtypes = [C.c_void_p]
     lib.bdpt_camera_load_settings.argtypes = [C.c_char_p, C.POINTER(Camera)]
+    lib.bdpt_camera_load_settings_lens.argtypes = [C.c_char_p, C.POINTER(Camera), C.POINTER(C.c_double),
+                                                   C.POINTER(C.c_double)]
     lib.bdpt_dae_free.restype = None
     lib.bdpt_exr_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                   C.POINTER(C.POINTER(C.c_float))]

@@ -1091,6 +1091,10 @@ int bdpt_dae_dump_json(const bdpt_dae* d, const char* path) {
 void bdpt_dae_free(bdpt_dae* d) { delete d; }
 
 int bdpt_camera_load_settings(const char* path, bdpt_camera* cam) {
+  return bdpt_camera_load_settings_lens(path, cam, nullptr, nullptr);
+}
+
+int bdpt_camera_load_settings_lens(const char* path, bdpt_camera* cam, double* focal_distance, double* lens_radius) {
   if (!path || !cam) { bdpt::g_err = "null argument"; return BDPT_E_INVALID; }
   std::ifstream file(path);
   if (!file.is_open()) { bdpt::g_err = std::string("cannot open camera settings ") + path; return BDPT_E_INVALID; }
@@ -1102,7 +1106,8 @@ int bdpt_camera_load_settings(const char* path, bdpt_camera* cam) {
   double c2w[3][3];   // (row, col)
   for (int i = 0; i < 9; ++i) c2w[i / 3][i % 3] = cam->c2w[3 * (i % 3) + i / 3];
   size_t screenW = 0, screenH = 0;
-  double screenDist = 0, focalDistance = 0, lensRadius = 0;
+  double screenDist = 0, focalDistance = focal_distance ? *focal_distance : 0,
+         lensRadius = lens_radius ? *lens_radius : 0;
   file >> hFov >> vFov >> ar >> nClip >> fClip;
   for (int i = 0; i < 3; ++i) file >> pos[i];
   for (int i = 0; i < 3; ++i) file >> target[i];
@@ -1116,6 +1121,8 @@ int bdpt_camera_load_settings(const char* path, bdpt_camera* cam) {
   cam->fclip = fClip;
   for (int i = 0; i < 3; ++i) cam->pos[i] = pos[i];
   for (int i = 0; i < 9; ++i) cam->c2w[3 * (i % 3) + i / 3] = c2w[i / 3][i % 3];   // column-major
+  if (focal_distance) *focal_distance = focalDistance;
+  if (lens_radius) *lens_radius = lensRadius;
   fprintf(stderr, "[Camera] Loaded settings from %s\n", path);
   return BDPT_OK;
 }

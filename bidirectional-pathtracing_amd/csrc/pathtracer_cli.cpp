@@ -49,6 +49,7 @@ void usage(const char* b) {
   printf("  --devices <LIST> Device of each of the -g workers, comma-separated (default 0..N-1)\n");
   printf("  -S  <INT>        RNG seed (default 5489)\n");
   printf("  --dump-scene <FILE>  Write the loaded scene as JSON\n");
+  printf("  --no-stats       Skip the ray / intersection-test counters of the end-of-render report\n");
   printf("  --tonemap <in.f64> <W> <H> <out.png>  Output stage only: raw float64 RGB (row 0 =\n"
          "                   bottom) -> PNG + _rate.png, as render_to_file writes them\n");
   printf("  -h               Print this help message\n");
@@ -67,7 +68,7 @@ int main(int argc, char** argv) {
   unsigned long long seed = 5489;
   std::string out, dump, scene, envpath, cam_settings;
   std::vector<int> devices;
-  bool rr = false, pt = false, hemi = false;
+  bool rr = false, pt = false, hemi = false, stats = true;
   int nal = 1, batch = 32;
   float tol = 0.05f;
   double lens = 0.0, focal = 4.7;
@@ -103,6 +104,7 @@ int main(int argc, char** argv) {
     else if (a == "--dump-scene") { need(1); dump = argv[++i]; }
     else if (a == "-e") { need(1); envpath = argv[++i]; }
     else if (a == "--rr") rr = true;
+    else if (a == "--no-stats") stats = false;
     else if (a == "--tonemap") {
       need(4);
       const int tw = atoi(argv[i + 2]), tht = atoi(argv[i + 3]);
@@ -134,8 +136,10 @@ int main(int argc, char** argv) {
   if (w <= 0 || h <= 0) { w = 800; h = 600; }
   bdpt_scene_desc desc;
   bdpt_dae_get_desc(dae, &desc);
-  // -c: after the -r resize, before rendering (main.cpp:172-178)
-  if (!cam_settings.empty() && bdpt_camera_load_settings(cam_settings.c_str(), &desc.camera) != BDPT_OK)
+  // -c: after the -r resize, before rendering (main.cpp:172-178); the file's focal distance and lens
+  // radius replace -d / -b, which set_camera gave the camera before (raytraced_renderer.cpp:141-142)
+  if (!cam_settings.empty() &&
+      bdpt_camera_load_settings_lens(cam_settings.c_str(), &desc.camera, &focal, &lens) != BDPT_OK)
     fprintf(stderr, "[PathTracer] %s (camera unchanged)\n", bdpt_last_error());
   bdpt_envmap env;
   float* env_rgb = nullptr;
@@ -154,6 +158,7 @@ int main(int argc, char** argv) {
   std::vector<int> rcs(gpus, 0);
   std::vector<std::vector<int32_t>> counts(gpus, std::vector<int32_t>((size_t)w * h, 0));
   std::vector<std::string> errs(gpus);
+  std::vector<bdpt_stats> st(gpus);
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int g = 0; g < gpus; g++) {
@@ -163,6 +168,7 @@ int main(int argc, char** argv) {
       p.width = w; p.height = h; p.spp = spp; p.max_depth = max_depth; p.seed = seed;
       p.device = g < (int)devices.size() ? devices[g] : g;
       p.russian_roulette = rr ? 1 : 0;
+      p.collect_stats = stats ? 1 : 0;
       if (pt) {
         p.integrator = BDPT_INTEGRATOR_PT;
         p.ns_area_light = nal; p.samples_per_batch = batch; p.max_tolerance = tol;
@@ -182,6 +188,7 @@ int main(int argc, char** argv) {
         rc = bdpt_render(ctx, mine.empty() ? nullptr : mine.data(), (int32_t)mine.size(), s0, s1 - s0);
       if (rc == BDPT_OK) rc = bdpt_read_frame(ctx, BDPT_FRAME_SAMPLE, frames[g].data());
       if (rc == BDPT_OK) rc = bdpt_read_sample_counts(ctx, counts[g].data());
+      if (rc == BDPT_OK && stats) rc = bdpt_get_stats(ctx, &st[g]);
       if (rc != BDPT_OK) errs[g] = bdpt_last_error();
       if (ctx) bdpt_destroy(ctx);
       rcs[g] = rc;
@@ -200,7 +207,21 @@ int main(int argc, char** argv) {
   for (int g = 1; g < gpus; g++)
     for (size_t k = 0; k < img.size(); k++) img[k] += frames[g][k];
   const double samples = (double)(tiles.empty() ? (long long)w * h : cdx * cdy) * spp;
-  fprintf(stderr, "[PathTracer] Rendering... 100%%! (%.4fs, %.2f Msamples/s)\n", secs, samples / secs / 1e6);
+  // the reference's end-of-render report (raytraced_renderer.cpp:679-682), on stdout: time, rays
+  // traced (closest-hit walk rays + connection rays), Mrays/s, primitive tests per ray
+  fprintf(stdout, "[PathTracer] Rendering... 100%%! (%.4fs)\n", secs);
+  if (stats) {
+    unsigned long long rays = 0, isects = 0;
+    for (int g = 0; g < gpus; g++) {
+      rays += st[g].rays;
+      isects += st[g].tri_tests + st[g].sph_tests;
+    }
+    fprintf(stdout, "[PathTracer] BVH traced %llu rays.\n", rays);
+    fprintf(stdout, "[PathTracer] Average speed %.4f million rays per second.\n", (double)rays / secs * 1e-6);
+    fprintf(stdout, "[PathTracer] Averaged %f intersection tests per ray.\n", rays ? (double)isects / rays : 0.0);
+  }
+  fflush(stdout);
+  fprintf(stderr, "[PathTracer] %.2f Msamples/s\n", samples / secs / 1e6);
   const std::vector<double> hdr(img.begin(), img.end());
   const std::vector<uint32_t> rgba = bdpt::tonemap(hdr.data(), w, h);
   fprintf(stderr, "[PathTracer] Saving to file: %s... ", out.c_str());

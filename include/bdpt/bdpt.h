@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 6
+#define BDPT_ABI_VERSION 7
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -264,6 +264,13 @@ void bdpt_dae_free(bdpt_dae* scene);
  * A file that cannot be opened leaves cam unchanged (as the reference's ifstream does) and returns
  * BDPT_E_INVALID. */
 int bdpt_camera_load_settings(const char* path, bdpt_camera* cam);
+/* ABI v7: the same, also returning the file's focalDistance and lensRadius (its last line), which
+ * Camera::load_settings writes over the thin-lens settings the renderer's config gave the camera
+ * (raytraced_renderer.cpp:141-142 set_camera runs first, main.cpp:177 load_camera after, and
+ * PathTracer::raytrace_pixel reads them in generate_ray_for_thin_lens, pathtracer.cpp:312).
+ * *focal_distance / *lens_radius carry the current values in (a short file leaves or zeroes them
+ * as the reference's extractions would). Either pointer may be null. */
+int bdpt_camera_load_settings_lens(const char* path, bdpt_camera* cam, double* focal_distance, double* lens_radius);
 
 /* Host-side OpenEXR reader for the -e environment map (main.cpp:40-77 load_exr, tinyexr):
  * scanline files with NONE / RLE / ZIPS / ZIP compression and HALF / FLOAT / UINT channels.

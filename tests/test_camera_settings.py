@@ -101,3 +101,50 @@ def test_cli_camera_settings(tmp_path):
     subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
     d = np.abs(ours.astype(int) - read_png(tmp_path / "ref.png").astype(int))
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
+
+
+def _lens_file(tmp_path, focal, lens, short=False):
+    """CBspheres_orbit.txt with its last line (focalDistance lensRadius) replaced, or dropped."""
+    lines = open(os.path.join(CAM, INDEX[KEY]["settings"])).read().strip().split("\n")
+    lines = lines[:-1] + ([] if short else [f"{focal} {lens}"])
+    p = tmp_path / "lens.txt"
+    p.write_text("\n".join(lines) + "\n")
+    return str(p)
+
+
+def test_settings_file_lens_replaces_config(tmp_path):
+    """Camera::load_settings reads focalDistance and lensRadius last (camera.cpp:184) and so
+    overwrites what set_camera took from -d / -b (raytraced_renderer.cpp:141-142); a file without
+    that line leaves the config's values (the failed extraction of a double at EOF stores 0 only
+    when characters were consumed; at EOF nothing is consumed and the members keep their values)."""
+    g = INDEX[KEY]
+    sc = B.load_dae(os.path.join(REPO, "scenes", g["scene"] + ".dae"), g["W"], g["H"])
+    assert sc.load_camera(_lens_file(tmp_path, 3.25, 0.125), 4.7, 0.0) == (3.25, 0.125)
+    sc = B.load_dae(os.path.join(REPO, "scenes", g["scene"] + ".dae"), g["W"], g["H"])
+    fd, lr = sc.load_camera(_lens_file(tmp_path, 0, 0, short=True), 4.5, 0.25)
+    assert (fd, lr) in ((4.5, 0.25), (0.0, 0.25))
+
+
+@pytest.mark.gpu
+def test_cli_pathtracer_uses_settings_file_lens(tmp_path):
+    """pathtracer --pt -c file: the thin lens of the file (not -b / -d) renders the image, as in the
+    reference (set_camera, then load_camera, then generate_ray_for_thin_lens, pathtracer.cpp:312)."""
+    from test_output_stage import CLI, read_png
+    from _util import oracle_pt_render
+    g = INDEX[KEY]
+    W, H, S, M = g["W"], g["H"], 4, 3
+    path = _lens_file(tmp_path, 3.25, 0.125)
+    sc = B.load_dae(os.path.join(REPO, "scenes", "CBspheres_lambertian.dae"), W, H)
+    fd, lr = sc.load_camera(path, 1.0, 0.0)
+    out = tmp_path / "pt.png"
+    r = subprocess.run([CLI, "--pt", "-s", str(S), "-m", str(M), "-a", str(S), "0.0", "-b", "0", "-d", "1",
+                        "-r", str(W), str(H), "-c", path, "-f", str(out),
+                        os.path.join(REPO, "scenes", "CBspheres_lambertian.dae")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    img, _, _ = oracle_pt_render(sc, W, H, S, M, MODE_C32, batch=S, tol=0.0, lens_radius=lr, focal_distance=fd)
+    raw = tmp_path / "ref.f64"
+    np.ascontiguousarray(img, dtype="<f8").tofile(raw)
+    subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
+    d = np.abs(read_png(out).astype(int) - read_png(tmp_path / "ref.png").astype(int))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size

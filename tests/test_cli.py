@@ -14,6 +14,21 @@ from test_output_stage import CLI, read_png
 pytestmark = pytest.mark.gpu
 
 
+def _check_report(stdout, samples):
+    """The reference's end-of-render report on stdout (raytraced_renderer.cpp:679-682), in the same
+    format: the regex bench.py uses on the reference binary must parse it, and the counters must be
+    those of this render (every pixel-sample traces at least its camera ray)."""
+    import re
+    m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", stdout)
+    assert m and float(m[-1]) > 0, stdout
+    rays = int(re.search(r"\[PathTracer\] BVH traced (\d+) rays\.", stdout).group(1))
+    assert rays >= samples
+    mrays = float(re.search(r"\[PathTracer\] Average speed ([0-9.]+) million rays per second\.", stdout).group(1))
+    assert abs(mrays - rays / float(m[-1]) * 1e-6) <= 1e-3 * mrays + 1e-3
+    tests = float(re.search(r"\[PathTracer\] Averaged ([0-9.]+) intersection tests per ray\.", stdout).group(1))
+    assert tests > 0
+
+
 def test_cli_renders_scene_like_oracle(tmp_path):
     W, H, S, M = 64, 48, 2, 5
     out = tmp_path / "cbs.png"
@@ -22,6 +37,7 @@ def test_cli_renders_scene_like_oracle(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Job completed" in r.stdout
+    _check_report(r.stdout, W * H * S)
     ours = read_png(out)
     ref_hdr = oracle_render(golden_scene("CBspheres", W, H), W, H, S, M, MODE_C32)[0]
     raw = tmp_path / "ref.f64"

@@ -421,3 +421,57 @@ def test_env_table_read_counters():
     assert st.samples == W * H * S
     assert st.env_samples > 0 and st.env_lookups > 0
     assert 0 < st.env_pdf_lookups <= st.env_lookups
+
+
+def test_c4_full_frame():
+    """Config C4's frame: CBgems 1920x1080, m=7 (the FOV quirk at 1080p, camera.cpp:83-89; splats
+    landing anywhere, bidirection.cpp:457-466; the scene whole in LDS, LM 1) at 1 spp vs the
+    oracle: sample, eye and light images each within the RMSE tolerance."""
+    W, H, S, M = 1920, 1080, 1, 7
+    sc = golden_scene("CBgems", W, H)
+    g = _gpu_render(sc, W, H, S, M, stats=True)
+    assert g["stats"].samples == W * H * S
+    _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32), "C4 CBgems 1920x1080 s1 m7")
+
+
+def test_c5_full_frame():
+    """Config C5's frame: the Lucy stand-in + the synthetic 1024x512 sky the bench uses (DESIGN.md
+    §9) at 1920x1080, m=8, Russian roulette on (the EXT kernel, compact pair lists) at 1 spp."""
+    W, H, S, M = 1920, 1080, 1, 8
+    sc = _with_env(_standin(W, H), 1024, 512)
+    g = _gpu_render(sc, W, H, S, M, rr=True, stats=True)
+    assert g["stats"].samples == W * H * S
+    _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32, rr=True), "C5 stand-in + env 1920x1080 s1 m8 RR")
+
+
+# Speculative traversal (bdpt_core.h spec_trav) descends with the ray's t before a postponed leaf
+# shrinks it, and an any-hit query may finish on a leaf after extra descent: the device visits a
+# superset of what one lane alone visits. Measured on the stand-in at 256x144 s1 m5 (LM 0 and 2):
+# node visits 1.0071x, triangle tests 1.0017x the replay's (profiles/r03_pytest_gpu.log).
+SPEC_EXCESS = 1.03
+
+
+@pytest.mark.parametrize("lds", ["2", "0"])
+def test_standin_counters_match_cpu_replay(lds, monkeypatch):
+    """The roofline's counters (N_node, N_tri per ray, counted in-kernel) against a
+    CPU replay of the same BVH4 traversal: bdpt_core.h compiled for the host (tests/native/core_cpu,
+    one lane, so no speculation) renders the same samples. Query and hit counts are equal (also to
+    the oracle's closest-hit queries and hits); node visits and triangle tests are at least the
+    replay's and at most SPEC_EXCESS times it."""
+    from test_core_cpu import core_render
+    monkeypatch.setenv("BDPT_LDS_MODE", lds)
+    W, H, S, M = 256, 144, 1, 5
+    sc = _standin(W, H)
+    st = _gpu_render(sc, W, H, S, M, stats=True)["stats"]
+    assert st.lds_mode == int(lds)
+    _, _, cs = core_render(sc, W, H, S, M, seed=5489, lds_mode=0)
+    o = oracle_render(sc, W, H, S, M, MODE_C32)[3]
+    assert st.samples == W * H * S
+    assert st.closest_rays == int(cs[1]) == int(o[1])
+    assert st.hits == int(cs[6]) == int(o[6])
+    assert st.shadow_rays == int(cs[2])
+    nodes, tris = int(cs[3]), int(cs[4])
+    print(f"LM {lds}: nodes gpu {st.node_visits} replay {nodes} ({st.node_visits / nodes:.4f}); "
+          f"tris gpu {st.tri_tests} replay {tris} ({st.tri_tests / tris:.4f})")
+    assert nodes <= st.node_visits <= SPEC_EXCESS * nodes
+    assert tris <= st.tri_tests <= SPEC_EXCESS * tris
