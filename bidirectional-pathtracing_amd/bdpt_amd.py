@@ -326,6 +326,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.bdpt_dae_get_desc.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
     lib.bdpt_dae_dump_json.argtypes = [C.c_void_p, C.c_char_p]
     lib.bdpt_dae_free.argtypes = [C.c_void_p]
+    lib.bdpt_read_frame_rect.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                         C.POINTER(C.c_float)]
     lib.bdpt_camera_load_settings.argtypes = [C.c_char_p, C.POINTER(Camera)]
     lib.bdpt_camera_load_settings_lens.argtypes = [C.c_char_p, C.POINTER(Camera), C.POINTER(C.c_double),
                                                    C.POINTER(C.c_double)]

@@ -1011,6 +1011,26 @@ int bdpt_read_frame(void* ctx, int32_t which, float* rgb) {
   return BDPT_OK;
 }
 
+int bdpt_read_frame_rect(void* ctx, int32_t which, int32_t x0, int32_t y0, int32_t w, int32_t h, float* rgb) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !rgb) { g_err = "null argument"; return BDPT_E_INVALID; }
+  const int W = c->prm.width, H = c->prm.height;
+  if (x0 < 0 || y0 < 0 || w < 0 || h < 0 || (int64_t)x0 + w > W || (int64_t)y0 + h > H) {
+    g_err = "rectangle outside the frame";
+    return BDPT_E_INVALID;
+  }
+  if (w == 0 || h == 0) return BDPT_OK;
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  void* p = nullptr;
+  int rc = bdpt_frame_device_ptr(ctx, which, &p);
+  if (rc) return rc;
+  const size_t row = (size_t)W * 3 * sizeof(float);
+  HIPCHK(hipMemcpy2DAsync(rgb, (size_t)w * 3 * sizeof(float), (const char*)p + ((size_t)y0 * W + x0) * 3 * sizeof(float), row,
+                          (size_t)w * 3 * sizeof(float), (size_t)h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return BDPT_OK;
+}
+
 int bdpt_read_sample_counts(void* ctx, int32_t* counts) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !counts) { g_err = "null argument"; return BDPT_E_INVALID; }

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 7
+#define BDPT_ABI_VERSION 8
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -218,6 +218,12 @@ int bdpt_sync(void* ctx);
 /* Copies a W*H*3 float frame (row 0 = bottom, as HDRImageBuffer) to host memory (sync). Under
  * the PathTracer, BDPT_FRAME_SAMPLE is its sampleBuffer (per-pixel means, update_pixel). */
 int bdpt_read_frame(void* ctx, int32_t which, float* rgb);
+
+/* ABI v8: the pixels [x0, x0 + w) x [y0, y0 + h) of a frame as w*h*3 floats, row 0 = y0 (sync):
+ * what a per-tile caller copies into sampleBuffer after raytrace_tile (the renderer reads the
+ * whole sampleBuffer through the non-virtual write_to_framebuffer after every tile,
+ * raytraced_renderer.cpp:619, pathtracer.cpp:42-45). The rectangle must lie inside the frame. */
+int bdpt_read_frame_rect(void* ctx, int32_t which, int32_t x0, int32_t y0, int32_t w, int32_t h, float* rgb);
 
 /* PathTracer::sampleCountBuffer (pathtracer.h:94): W*H samples per pixel, row 0 = bottom (sync).
  * Under BDPT every rendered pixel reports the samples rendered for it. */

@@ -3,11 +3,27 @@
 // libbdpt_amd.so (include/bdpt/bdpt.h). INTEGRATION.md walks through it.
 //
 // BidirectionalPathTracerAMD replaces BidirectionalPathTracer (bidirection.h:51-92) behind the
-// PathTracer interface (pathtracer.h:23-104): RaytracedRenderer creates it at
-// raytraced_renderer.cpp:53, calls attach() where build_accel collects the primitives
-// (raytraced_renderer.cpp:350-374), its workers call raytrace_tile() per tile (:595-620) — or one
-// thread renders the whole frame with raytrace_frame() — and finish() copies the frame into
-// sampleBuffer before save_image. raytrace_pixel() stays available as a 1x1 tile.
+// PathTracer interface (pathtracer.h:23-104). The one change to the reference is the class the
+// renderer constructs (raytraced_renderer.cpp:53):
+//     -  pt = new BidirectionalPathTracer();
+//     +  pt = new BidirectionalPathTracerAMD();
+// Everything else — render_to_file, start_raytracing, the worker threads' raytrace_tile loop of
+// raytrace_pixel calls, write_to_framebuffer after every tile, save_image — runs unmodified:
+//   * start_raytracing calls clear() and set_frame_size(), then sets bvh / camera / scene
+//     (:280-285); the first raytrace_pixel() of the frame attaches the scene (bdpt_create over
+//     scene->objects' primitives in build_accel's collection order, scene->lights, *camera and
+//     envLight's map);
+//   * the workers call raytrace_pixel() per pixel of a 32x32 tile, row-major (:293-298, 610-615):
+//     the tile's first pixel renders the whole tile with ONE bdpt_render and copies the tile's
+//     pixels of the device frame into sampleBuffer (and sampleCountBuffer = ns_aa, as
+//     bidirection.cpp:539), the others are no-ops, so the write_to_framebuffer after the tile
+//     (:619, non-virtual, pathtracer.cpp:42-45) shows it;
+//   * when the last pixel of the frame has been rendered the whole frame — light-tracing splats
+//     land anywhere (bidirection.cpp:457-466) — goes to sampleBuffer / eyeBuffer / lightBuffer,
+//     so the last write_to_framebuffer and save_image see the final image.
+// A pixel that no 32x32 tile covers (the -p cell path, 8x8 tiles at an arbitrary corner) is a 1x1
+// tile. attach() / raytrace_tile() / raytrace_frame() / finish() remain for callers that drive
+// whole tiles or frames themselves.
 //
 // Flattening reads the reference's scene objects: Triangle p1..p3 / n1..n3, Sphere o / r, the
 // BSDF parameters, the light fields and the camera (hFov, vFov, nClip, fClip, pos, c2w, w2c). The
@@ -16,13 +32,18 @@
 // compile check in tests/test_integration.py builds it with the same read access the oracle's
 // ref_driver uses.
 //
-// Threading: the reference's worker threads may call raytrace_tile concurrently; bdpt_render locks
-// its context, so concurrent tiles are serialised on the GPU queue (include/bdpt/bdpt.h).
+// Threading: the reference's worker threads call raytrace_pixel concurrently (on disjoint tiles);
+// the binding's tile bookkeeping is under a mutex, and bdpt_render serialises launches per context.
 #ifndef BDPT_AMD_INTEGRATION_BIDIRECTION_AMD_H
 #define BDPT_AMD_INTEGRATION_BIDIRECTION_AMD_H
 
+#include <algorithm>
+#include <atomic>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "bdpt/bdpt.h"
@@ -117,24 +138,98 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     return bdpt_create(&desc, &p, &ctx_);
   }
 
-  void raytrace_pixel(size_t x, size_t y) override {   // the reference's per-pixel entry: a 1x1 tile
-    raytrace_tile((int)x, (int)y, 1, 1);
+  // ---- the PathTracer contract, driven by the reference's unmodified RaytracedRenderer ----
+  void set_frame_size(size_t width, size_t height) override {
+    BidirectionalPathTracer::set_frame_size(width, height);
+    drop_frame();
   }
+  // The renderer's per-pixel call (raytraced_renderer.cpp:610-615; bidirection.cpp:503-542). It
+  // runs on the renderer's worker threads, where an exception would end the process, so a failure
+  // (no device, bdpt_* error) is recorded — error() — and the frame's remaining pixels are skipped.
+  void raytrace_pixel(size_t x, size_t y) override {
+    const size_t W = sampleBuffer.w, H = sampleBuffer.h;
+    if (x >= W || y >= H || failed_.load(std::memory_order_acquire)) return;
+    if (done_ && done_[x + y * W].load(std::memory_order_acquire)) return;   // rendered with its tile
+    std::lock_guard<std::mutex> lk(mu_);
+    if (failed_.load(std::memory_order_relaxed)) return;
+    try {
+      render_pixel_locked(x, y, W, H);
+    } catch (const std::exception& e) {
+      err_ = e.what();
+      failed_.store(true, std::memory_order_release);
+    }
+  }
+  // empty, or the first failure of the frame's raytrace_pixel calls
+  std::string error() const { return failed_.load() ? err_ : std::string(); }
+  size_t launches() const { return launches_; }   // bdpt_render calls since the last frame reset
+
+ private:
+  void render_pixel_locked(size_t x, size_t y, size_t W, size_t H) {
+    if (!ctx_) {
+      if (!scene || !camera) throw std::runtime_error("BidirectionalPathTracerAMD: no scene / camera");
+      std::vector<SceneObjects::Primitive*> prims;   // build_accel's collection order (:352-360)
+      for (SceneObjects::SceneObject* obj : scene->objects) {
+        const std::vector<SceneObjects::Primitive*>& op = obj->get_primitives();
+        prims.insert(prims.end(), op.begin(), op.end());
+      }
+      const HDRImageBuffer* env = envLight ? static_cast<const SceneObjects::EnvironmentLight*>(envLight)->envMap : nullptr;
+      check(attach(prims, scene->lights, *camera, env));
+    }
+    if (!done_) {
+      done_.reset(new std::atomic<uint8_t>[W * H]);
+      for (size_t k = 0; k < W * H; k++) done_[k].store(0, std::memory_order_relaxed);
+      rendered_ = 0;
+    }
+    if (done_[x + y * W].load(std::memory_order_relaxed)) return;
+    // the tile whose first pixel this is (tiles start at multiples of imageTileSize = 32,
+    // raytraced_renderer.cpp:83,293-298), else this pixel alone
+    const bool corner = x % kTile == 0 && y % kTile == 0;
+    const size_t tw = corner ? std::min(kTile, W - x) : 1, th = corner ? std::min(kTile, H - y) : 1;
+    raytrace_tile((int)x, (int)y, (int)tw, (int)th);
+    for (size_t yy = y; yy < y + th; yy++)
+      for (size_t xx = x; xx < x + tw; xx++) {
+        sampleCountBuffer[xx + yy * W] = ns_aa;   // bidirection.cpp:539
+        if (!done_[xx + yy * W].exchange(1, std::memory_order_release)) rendered_++;
+      }
+    if (rendered_ == W * H) {
+      finish();   // the frame is complete: every splat is in, sampleBuffer <- the whole image
+    } else {
+      std::vector<float> rgb(tw * th * 3);
+      check(bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, (int32_t)x, (int32_t)y, (int32_t)tw, (int32_t)th, rgb.data()));
+      for (size_t yy = 0; yy < th; yy++)
+        for (size_t xx = 0; xx < tw; xx++) {
+          const float* v = &rgb[3 * (xx + yy * tw)];
+          sampleBuffer.data[(x + xx) + (y + yy) * W] = Vector3D(v[0], v[1], v[2]);
+        }
+    }
+  }
+
+ public:
   void raytrace_tile(int tx, int ty, int w, int h) {    // RaytracedRenderer::raytrace_tile's unit
     bdpt_tile t = {tx, ty, w, h};
     check(bdpt_render(ctx_, &t, 1, 0, (int32_t)ns_aa));
+    launches_++;
   }
-  void raytrace_frame() { check(bdpt_render(ctx_, nullptr, 0, 0, (int32_t)ns_aa)); }
+  void raytrace_frame() {
+    check(bdpt_render(ctx_, nullptr, 0, 0, (int32_t)ns_aa));
+    launches_++;
+  }
+  // start_raytracing (:280) clears before every frame: the next raytrace_pixel attaches again
   void clear() override {
     BidirectionalPathTracer::clear();
-    if (ctx_) check(bdpt_clear(ctx_));
+    drop_frame();
   }
-  // sampleBuffer <- the device frame (eyeBuffer + lightBuffer), before save_image
+  // sampleBuffer / eyeBuffer / lightBuffer <- the device frames, before save_image
   void finish() {
-    std::vector<float> rgb(sampleBuffer.w * sampleBuffer.h * 3);
-    check(bdpt_read_frame(ctx_, BDPT_FRAME_SAMPLE, rgb.data()));
-    for (size_t k = 0; k < sampleBuffer.w * sampleBuffer.h; k++)
-      sampleBuffer.data[k] = Vector3D(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+    const size_t n = sampleBuffer.w * sampleBuffer.h;
+    std::vector<float> rgb(n * 3);
+    HDRImageBuffer* dst[3] = {&sampleBuffer, &eyeBuffer, &lightBuffer};
+    const int32_t which[3] = {BDPT_FRAME_SAMPLE, BDPT_FRAME_EYE, BDPT_FRAME_LIGHT};
+    for (int b = 0; b < 3; b++) {
+      if (dst[b]->w * dst[b]->h != n) continue;
+      check(bdpt_read_frame(ctx_, which[b], rgb.data()));
+      for (size_t k = 0; k < n; k++) dst[b]->data[k] = Vector3D(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+    }
   }
   ~BidirectionalPathTracerAMD() {
     if (ctx_) bdpt_destroy(ctx_);
@@ -165,6 +260,15 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     }
     return m;
   }
+  void drop_frame() {   // a new frame (size / scene / camera may have changed): attach again
+    std::lock_guard<std::mutex> lk(mu_);
+    if (ctx_) { bdpt_destroy(ctx_); ctx_ = nullptr; }
+    done_.reset();
+    rendered_ = 0;
+    launches_ = 0;
+    failed_.store(false);
+    err_.clear();
+  }
   static bdpt_camera camera_desc(const Camera& c) {   // camera.h:104-125
     bdpt_camera d = {};
     copy3(d.pos, c.pos);
@@ -180,7 +284,13 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     return d;
   }
 
+  static constexpr size_t kTile = 32;   // RaytracedRenderer::imageTileSize (raytraced_renderer.cpp:83)
   void* ctx_ = nullptr;
+  std::mutex mu_;
+  std::unique_ptr<std::atomic<uint8_t>[]> done_;   // per pixel: rendered with its tile
+  size_t rendered_ = 0, launches_ = 0;
+  std::atomic<bool> failed_{false};
+  std::string err_;
   std::vector<int32_t> type_, mat_;
   std::vector<double> geom_;
   std::vector<bdpt_material> mats_;

@@ -246,10 +246,10 @@ int main(int argc, char** argv) {
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
   std::string png = "/dev/null", npy_prefix, scene_json, cam_settings;
-  bool render = true, uni = false, amd = false;
+  bool render = true, uni = false, amd = false, amd_loop = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:G")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GA")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -268,6 +268,7 @@ int main(int argc, char** argv) {
       case 'a': batch = atoi(argv[optind - 1]); tol = atof(argv[optind]); optind++; break;   // main.cpp:134-137
       case 'c': cam_settings = optarg; break;            // main.cpp:120-121
       case 'G': amd = true; break;                       // integration check (BDPT_INTEGRATION builds)
+      case 'A': amd_loop = true; break;                  // the binding under the reference's own render loop
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -353,6 +354,28 @@ int main(int argc, char** argv) {
     u->direct_hemisphere_sample = b->direct_hemisphere_sample; u->envLight = b->envLight;
     rr->pt = u;
   }
+#ifdef BDPT_INTEGRATION
+  BidirectionalPathTracerAMD* amd_pt = nullptr;
+  if (amd_loop) {
+    // The integration's one-line change at raytraced_renderer.cpp:53 — the renderer holds a
+    // BidirectionalPathTracerAMD instead of a BidirectionalPathTracer, with the same settings
+    // (:55-75) — made here right after construction; set_camera / set_scene / set_frame_size and
+    // render_to_file (worker threads, raytrace_tile -> raytrace_pixel, write_to_framebuffer,
+    // save_image) below run as the reference wrote them.
+    PathTracer* b = rr->pt;
+    amd_pt = new BidirectionalPathTracerAMD();
+    amd_pt->ns_aa = b->ns_aa; amd_pt->max_ray_depth = b->max_ray_depth; amd_pt->ns_area_light = b->ns_area_light;
+    amd_pt->ns_diff = b->ns_diff; amd_pt->ns_glsy = b->ns_glsy; amd_pt->ns_refr = b->ns_refr;
+    amd_pt->samplesPerBatch = b->samplesPerBatch; amd_pt->maxTolerance = b->maxTolerance;
+    amd_pt->direct_hemisphere_sample = b->direct_hemisphere_sample; amd_pt->envLight = b->envLight;
+    rr->pt = amd_pt;
+  }
+#else
+  if (amd_loop) {
+    fprintf(stderr, "[ref_driver] -A needs the BDPT_INTEGRATION build (oracle/_ref/ref_driver_amd)\n");
+    return 2;
+  }
+#endif
   // --- set_up_pathtracer (application.cpp:633-639) ---
   rr->set_camera(&camera);
   rr->set_scene(scene->get_static_scene());
@@ -389,7 +412,19 @@ int main(int argc, char** argv) {
     return 2;
 #endif
   }
-  rr->render_to_file(png, (size_t)-1, 0, 0, 0);
+  try {
+    rr->render_to_file(png, (size_t)-1, 0, 0, 0);
+  } catch (const std::exception& e) {   // the binding reports bdpt_* failures as exceptions
+    fprintf(stderr, "[ref_driver] %s\n", e.what());
+    return 23;
+  }
+#ifdef BDPT_INTEGRATION
+  if (amd_pt && !amd_pt->error().empty()) {
+    fprintf(stderr, "[ref_driver] BidirectionalPathTracerAMD: %s\n", amd_pt->error().c_str());
+    return amd_pt->error() == "no HIP device" ? 23 : 24;
+  }
+  if (amd_pt) fprintf(stdout, "[ref_driver] bdpt_render launches: %zu\n", amd_pt->launches());
+#endif
   if (!npy_prefix.empty() && uni) {
     write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);
     FILE* fc = fopen((npy_prefix + "_count.bin").c_str(), "wb");   // sampleCountBuffer, int32 row-major

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_function():
 
 
 def test_abi_version():
-    assert B.load_library().bdpt_abi_version() == 7   # v2: envmap + RR; v3: integrator; v4: LDS stats; v5: camera settings; v6: env-table stats; v7: camera lens settings
+    assert B.load_library().bdpt_abi_version() == 8   # v2: envmap + RR; v3: integrator; v4: LDS stats; v5: camera settings; v6: env-table stats; v7: camera lens settings; v8: frame rectangles
 
 
 def test_null_arguments_rejected():

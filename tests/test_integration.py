@@ -53,3 +53,61 @@ def test_binding_renders_like_the_oracle(tmp_path, scene, M):
     ref = oracle_render(sc, W, H, S, M, MODE_C32)[0]
     rmse = float(np.sqrt(np.mean((ours - ref) ** 2)))
     assert rmse < 1e-4, rmse
+
+
+def _run_loop(tmp_path, scene, W, H, S, M, threads=8):
+    """-A: the binding behind the reference's own render loop (RaytracedRenderer::render_to_file with
+    `threads` workers -> raytrace_tile -> raytrace_pixel -> write_to_framebuffer -> save_image), with
+    the one-line swap of raytraced_renderer.cpp:53 done right after the renderer is constructed."""
+    prefix = str(tmp_path / "loop")
+    png = str(tmp_path / "loop.png")
+    r = subprocess.run([AMD, "-A", "-t", str(threads), "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-f", png,
+                        "-o", prefix, os.path.join(REPO, "scenes", scene + ".dae")], capture_output=True, text=True,
+                       timeout=300, cwd=tmp_path)
+    return r, png, prefix
+
+
+@needs_bin
+def test_render_loop_binding_fails_cleanly_without_device(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present: the GPU test covers the binding")
+    r, _, _ = _run_loop(tmp_path, "CBspheres", 64, 48, 2, 5)
+    assert r.returncode == 23, r.stdout + r.stderr
+    assert "no HIP device" in r.stderr
+
+
+@needs_bin
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,W,H,S,M", [("CBspheres", 200, 150, 2, 5), ("CBgems", 160, 100, 2, 7)])
+def test_reference_render_loop_through_binding(tmp_path, scene, W, H, S, M):
+    """The reference's unmodified render_to_file at -t 8 with BidirectionalPathTracerAMD in place:
+    one bdpt_render per 32x32 tile (raytraced_renderer.cpp:293-298), the PNG its own save_image
+    writes equal to the product CLI's at the same seed (light-image splats are fp32 atomics in
+    another order, so a byte may differ by one step where a value sits on a quantisation
+    boundary), its sampleBuffer / eyeBuffer / lightBuffer within the parity tolerance of the
+    oracle's mode 2, and its sampling-rate image all ns_aa (bidirection.cpp:539)."""
+    import bdpt_amd as B
+    from test_output_stage import CLI, read_png
+    r, png, prefix = _run_loop(tmp_path, scene, W, H, S, M)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Rendering... 100%!" in r.stdout and "Job completed" in r.stdout
+    ntiles = ((W + 31) // 32) * ((H + 31) // 32)
+    launches = int(r.stdout.split("bdpt_render launches:")[1].split()[0])
+    assert launches == ntiles, (launches, ntiles)
+    sc = B.load_dae(os.path.join(REPO, "scenes", scene + ".dae"), W, H)
+    samp, eye, light, _ = oracle_render(sc, W, H, S, M, MODE_C32)
+    for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
+        ours = np.load(f"{prefix}_{name}.npy")
+        rmse = float(np.sqrt(np.mean((ours - ref) ** 2)))
+        assert rmse < 1e-4, (name, rmse)
+    cli_png = tmp_path / "cli.png"
+    rc = subprocess.run([CLI, "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-f", str(cli_png), "--no-stats",
+                         os.path.join(REPO, "scenes", scene + ".dae")], capture_output=True, text=True, timeout=300)
+    assert rc.returncode == 0, rc.stderr
+    a, b = read_png(png).astype(int), read_png(cli_png).astype(int)
+    d = np.abs(a - b)
+    print(f"{scene}: PNG bytes differing {np.count_nonzero(d)} of {d.size}, max {d.max()}")
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.001 * d.size
+    rate_ref = read_png(tmp_path / "loop_rate.png")
+    assert np.array_equal(rate_ref, read_png(tmp_path / "cli_rate.png"))
