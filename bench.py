@@ -76,6 +76,19 @@ def env_bytes(st) -> int:
             + BYTES_ENV_PDF * st.env_pdf_lookups)
 
 
+# What the kernel's loads actually request (bdpt_core.h): a 4-wide node is 7 float4 (112 B) for 4
+# children = 28 B per child AABB (LDS modes 0 / 2), a 2-wide node 4 float4 for 2 = 32 B (modes 1 /
+# 3); a primitive test loads its whole 48-B record (3 float4, software-pipelined); a closest hit
+# its 48-B shading record.
+FETCH_NODE_CHILD = {0: 28, 1: 32, 2: 28, 3: 32}
+FETCH_PRIM, FETCH_HIT = 48, 48
+
+
+def fetched_bytes(st) -> int:
+    return (FETCH_NODE_CHILD.get(st.lds_mode, 32) * st.node_visits + FETCH_PRIM * (st.tri_tests + st.sph_tests)
+            + FETCH_HIT * st.hits + env_bytes(st))
+
+
 def global_memory_bytes(st) -> int:
     """The algorithmic bytes minus what the kernel read from the CU's LDS copy of the scene (the
     BFS treelet in LDS mode 2; the whole scene in modes 1 / 3): the part that has to come through
@@ -181,9 +194,15 @@ def load_traffic(workload: str, kernel_ms: float):
     if not b:
         return None, None
     gbps = b / (kernel_ms * 1e-3) / 1e9
-    return b, {"source": os.path.relpath(path, REPO), "read_bytes": rec.get("hbm_read_bytes"),
-               "write_bytes": rec.get("hbm_write_bytes"), "gbps_at_this_kernel_ms": round(gbps, 2),
-               "frac": round(gbps / HBM_PEAK_GBPS, 5), "pmc_kernel_ms": rec.get("kernel_ms")}
+    pms = rec.get("kernel_ms")
+    info = {"source": os.path.relpath(path, REPO), "read_bytes": rec.get("hbm_read_bytes"),
+            "write_bytes": rec.get("hbm_write_bytes"), "read_bytes_x2_upper": rec.get("hbm_read_bytes_x2_upper"),
+            "gbps_at_this_kernel_ms": round(gbps, 2), "frac_at_this_kernel_ms": round(gbps / HBM_PEAK_GBPS, 5),
+            "pmc_kernel_ms": pms}
+    if pms:   # the bytes over the duration of the dispatch they were counted on (same rocprofv3 run)
+        info["pmc_gbps"] = round(b / (pms * 1e-3) / 1e9, 2)
+        info["pmc_frac"] = round(b / (pms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)
+    return b, info
 
 
 def main() -> int:
@@ -335,6 +354,7 @@ def main() -> int:
     ps.close()
     bytes_launch = algorithmic_bytes(st)
     gmem_launch = global_memory_bytes(st)
+    fetched_launch = fetched_bytes(st)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = samples_per_step * args.steps / elapsed / 1e6
     traffic, traffic_info = (None, None)
@@ -378,11 +398,17 @@ def main() -> int:
                      "traffic": traffic, "kernel": "k_pt" if use_pt else "k_bdpt_sample",
                      "kernel_ms": round(kern_ms, 3),
                      "algorithmic_bytes_per_launch": bytes_launch,
-                     "note": "achieved = SURVEY §8d algorithmic scene bytes (32 B/child AABB, 36 B/triangle "
-                             "test, 16 B/sphere test, 40 B/closest hit; environment light: 76 B/sampled "
-                             "direction, 48 B/radiance lookup, 4 B/pdf lookup) / launch time (HIP events on "
-                             "the ctx stream); gmem_* leaves out the scene reads served from the CU's LDS "
-                             "copy; traffic = measured HBM-side bytes (PMC)",
+                     "note": "achieved / frac = SURVEY §8d algorithmic scene bytes (its convention: 32 B/child "
+                             "AABB, 36 B/triangle test, 16 B/sphere test, 40 B/closest hit; environment light: "
+                             "76 B/sampled direction, 48 B/radiance lookup, 4 B/pdf lookup) / launch time (HIP "
+                             "events on the ctx stream); fetched_* = the bytes the loads request (28 B/child of a "
+                             "4-wide node, 32 B/child of a 2-wide one, 48 B/primitive record, 48 B/shading "
+                             "record); gmem_* = the §8d bytes minus the scene reads served from the CU's LDS "
+                             "copy (the part that goes through L2 / HBM); traffic = measured HBM-side bytes "
+                             "(PMC FETCH_SIZE + WRITE_SIZE, traffic_pmc.pmc_frac over the dispatch they were "
+                             "counted on)",
+                     "fetched_bytes_per_launch": fetched_launch,
+                     "frac_fetched_bytes": round(fetched_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
                      "gmem_bytes_per_launch": gmem_launch,
                      "gmem_achieved": round(gmem_launch / (kern_ms * 1e-3) / 1e9, 2),
                      "gmem_frac": round(gmem_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """OUT_DIR/traffic_<workload>.json (then copied to profiles/) from the FETCH_SIZE / WRITE_SIZE passes of a GPU session
-(tools/gpu_session_r02.sh): HBM-side bytes of the largest k_bdpt_sample dispatch, i.e. one
-bench-sized launch of the workload (tools/prof_render.py). FETCH_SIZE / WRITE_SIZE are in KB
-(MI355X_MICROARCH.md, HBM section). The guide's x2 FETCH correction is calibrated for 16-B/lane
-streaming reads only; this kernel's memory-side reads are gathers (BVH nodes, primitives), scratch
-(path vertices, spilled registers) and frame atomics, so the raw value is reported as traffic and the
-x2 figure as an upper bound.
-usage: pmc_traffic.py OUT_DIR WORKLOAD_KEY "description" [kernel_stats.csv]"""
+(tools/gpu_session_r03.sh): HBM-side bytes of the largest k_bdpt_sample dispatch, i.e. one
+bench-sized launch of the workload (tools/prof_render.py), and that dispatch's duration from the
+kernel trace collected in the same rocprofv3 run (--pmc with --kernel-trace), so the bytes are tied
+to a measured kernel time. FETCH_SIZE / WRITE_SIZE are in KB (MI355X_MICROARCH.md, HBM section).
+The guide's x2 FETCH correction is calibrated for 16-B/lane streaming reads only; this kernel's
+memory-side reads are gathers (BVH nodes, primitives), scratch (path vertices, spilled registers)
+and frame atomics, so the raw value is reported as traffic and the x2 figure as an upper bound.
+usage: pmc_traffic.py OUT_DIR WORKLOAD_KEY "description" """
 import csv
 import glob
 import json
@@ -21,8 +22,17 @@ def biggest(d, counter):
             if "k_bdpt_sample" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 v = float(r["Counter_Value"])
                 if best is None or v > best[0]:
-                    best = (v, r["Kernel_Name"], int(r["Grid_Size"]))
+                    best = (v, r["Kernel_Name"], r.get("Dispatch_Id"))
     return best
+
+
+def dispatch_ms(d, kernel, dispatch):
+    """Duration of that dispatch in the same run's kernel trace (None without one)."""
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Kernel_Name") == kernel and (dispatch is None or r.get("Dispatch_Id") == dispatch):
+                return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return None
 
 
 def main():
@@ -31,6 +41,8 @@ def main():
     write = biggest(os.path.join(out, "pmc_write"), "WRITE_SIZE")
     if fetch is None or write is None:
         sys.exit("no k_bdpt_sample FETCH_SIZE / WRITE_SIZE rows found under " + out)
+    fms = dispatch_ms(os.path.join(out, "pmc_fetch"), fetch[1], fetch[2])
+    wms = dispatch_ms(os.path.join(out, "pmc_write"), write[1], write[2])
     rec = {
         "workload": desc,
         "workload_key": key,
@@ -39,13 +51,12 @@ def main():
         "hbm_read_bytes": fetch[0] * 1024, "hbm_write_bytes": write[0] * 1024,
         "hbm_bytes_per_launch": (fetch[0] + write[0]) * 1024,
         "hbm_read_bytes_x2_upper": 2 * fetch[0] * 1024,
-        "note": "FETCH_SIZE/WRITE_SIZE in KB, one launch, separate --pmc passes; x2 FETCH correction "
-                "(16-B streaming reads) not applied",
+        "fetch_pass_kernel_ms": fms, "write_pass_kernel_ms": wms,
+        "kernel_ms": (fms + wms) / 2 if fms and wms else None,
+        "note": "FETCH_SIZE/WRITE_SIZE in KB, one launch, separate --pmc passes each with its own kernel "
+                "trace (kernel_ms = mean of the two dispatch durations); x2 FETCH correction (16-B "
+                "streaming reads) not applied",
     }
-    if len(sys.argv) > 4 and os.path.exists(sys.argv[4]):   # the same launch's duration, kernel trace
-        for r in csv.DictReader(open(sys.argv[4])):
-            if r["Name"] == fetch[1]:
-                rec["kernel_ms"] = float(r["AverageNs"]) / 1e6
     path = os.path.join(out, f"traffic_{key}.json")   # copied into profiles/ after the session
     with open(path, "w") as f:
         json.dump(rec, f, indent=1)
