@@ -1722,6 +1722,14 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         prev_n = n;
         nalpha = next_alpha(v.alpha, n, rd, fv, pdf * q);
         i++;
+        // A subpath whose throughput is exactly zero (the vertex's f = 0: an emitter, a diffuse
+        // surface seen from behind, bsdf.cpp:56-58,99-110) would walk on to the depth cap with
+        // alpha = 0: every later vertex has alpha = 0, so no
+        // connection can use it (can_connect, make_conn's contrib gate) and no weight of another
+        // connection reads it, and the walk's draws come from its own counter stream. Ending it
+        // here is output-identical (tests/test_core_cpu.py vs the oracle, which walks on) and
+        // saves 3-4% of the walk rays at the north star's 1080p FOV.
+        if (!nonzero3(nalpha)) end = true;
       }
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
       cnt.clk_vertex += __builtin_amdgcn_s_memtime() - tq1;

@@ -90,16 +90,19 @@ def test_tiles_and_sample_ranges_compose(pipe):
 @pytest.mark.parametrize("pipe", PIPES)
 def test_stats_counters_match_oracle(pipe):
     """In-kernel counters (roofline bytes) against the oracle's counts of the same traversal work:
-    closest-hit queries and hits are identical; the device skips zero-contribution connection rays
-    and culls boxes, so shadow rays / node visits are <= the oracle's."""
+    the device skips zero-contribution connection rays, the rest of a zero-throughput walk
+    (megakernel, bdpt_core.h prepare_sample) and culls boxes, so its closest-hit queries, hits,
+    shadow rays and node visits are <= the oracle's (which walks on, as the reference does)."""
     W, H, S, M = 64, 48, 2, 5
     sc = golden_scene("CBspheres", W, H)
     g = _gpu_render(sc, W, H, S, M, stats=True, pipeline=pipe)
     st = g["stats"]
     o = oracle_render(sc, W, H, S, M, MODE_C32)[3]
     assert st.samples == W * H * S
-    assert st.closest_rays == int(o[1])
-    assert st.hits == int(o[6])
+    assert 0.9 * int(o[1]) <= st.closest_rays <= int(o[1])
+    assert 0.9 * int(o[6]) <= st.hits <= int(o[6])
+    if pipe == B.PIPELINE_WAVEFRONT:   # walks on to the depth cap, as the oracle
+        assert st.closest_rays == int(o[1]) and st.hits == int(o[6])
     assert 0 < st.shadow_rays <= int(o[2])
     assert 0 < st.tri_tests + st.sph_tests
     # the megakernel runs this 14-primitive scene with the flat leaf list (no node fetches)
@@ -457,7 +460,8 @@ def test_standin_counters_match_cpu_replay(lds, monkeypatch):
     CPU replay of the same BVH4 traversal: bdpt_core.h compiled for the host (tests/native/core_cpu,
     one lane, so no speculation) renders the same samples. Query and hit counts are equal (also to
     the oracle's closest-hit queries and hits); node visits and triangle tests are at least the
-    replay's and at most SPEC_EXCESS times it."""
+    replay's and at most SPEC_EXCESS times it. (The oracle walks zero-throughput subpaths on to the
+    depth cap, as the reference does; the device ends them: its counts are <= the oracle's.)"""
     from test_core_cpu import core_render
     monkeypatch.setenv("BDPT_LDS_MODE", lds)
     W, H, S, M = 256, 144, 1, 5
@@ -467,8 +471,8 @@ def test_standin_counters_match_cpu_replay(lds, monkeypatch):
     _, _, cs = core_render(sc, W, H, S, M, seed=5489, lds_mode=0)
     o = oracle_render(sc, W, H, S, M, MODE_C32)[3]
     assert st.samples == W * H * S
-    assert st.closest_rays == int(cs[1]) == int(o[1])
-    assert st.hits == int(cs[6]) == int(o[6])
+    assert st.closest_rays == int(cs[1]) <= int(o[1])
+    assert st.hits == int(cs[6]) <= int(o[6])
     assert st.shadow_rays == int(cs[2])
     nodes, tris = int(cs[3]), int(cs[4])
     print(f"LM {lds}: nodes gpu {st.node_visits} replay {nodes} ({st.node_visits / nodes:.4f}); "
