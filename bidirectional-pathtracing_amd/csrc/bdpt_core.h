@@ -357,30 +357,20 @@ namespace bdpt {
 
 // ------------------------------------------------------------------------------------------------
 // BVH traversal (replaces BVHAccel::intersect, bvh.cpp:161-188; see header comment).
-#ifndef BDPT_STACK
-#define BDPT_STACK 64
-#endif
+constexpr int kStackMax = 64;
 // Register-stack entries of the megakernel's walk / connection-ray traversals (TravStack<K>).
 // Measured (Lucy stand-in 1080p / CBspheres / CBgems, Msamples/s): K 0: 440 / 438 / 273,
 // K 2: 465 / 452 / 284, K 4: 465 / 450 / 290 (walk 8 or connection 8: no further gain).
-#ifndef BDPT_WALK_STACK
-#define BDPT_WALK_STACK 4
-#endif
-#ifndef BDPT_CONN_STACK
-#define BDPT_CONN_STACK 4
-#endif
+constexpr int kWalkStack = 4;
+constexpr int kConnStack = 4;
 // Children per BVH node: 2 (64-B nodes) or 4 (128-B nodes: half the dependent node fetches per
 // ray, four independent slab tests per fetch). The host emits both trees over the same leaves;
 // a kernel traverses the one its LDS mode selects: scenes fetched from HBM (LM 0, LM 2's nodes below
 // the treelet) gain from the shorter dependent chain, a scene held whole in LDS (LM 1) does not
 // (its fetches are short, and the wider test costs instructions). Measured, DESIGN.md §5.
-#ifndef BDPT_BVH_WIDTH
-#define BDPT_BVH_WIDTH 4       // LM 0 / 2
-#endif
-#ifndef BDPT_LDS_BVH_WIDTH
-#define BDPT_LDS_BVH_WIDTH 2   // LM 1
-#endif
-static_assert((BDPT_BVH_WIDTH == 2 || BDPT_BVH_WIDTH == 4) && (BDPT_LDS_BVH_WIDTH == 2 || BDPT_LDS_BVH_WIDTH == 4),
+constexpr int kBvhWidth = 4;       // LM 0 / 2
+constexpr int kLdsBvhWidth = 2;   // LM 1
+static_assert((kBvhWidth == 2 || kBvhWidth == 4) && (kLdsBvhWidth == 2 || kLdsBvhWidth == 4),
               "BVH widths must be 2 or 4");
 // Child visiting order of the 4-wide node step: 0 = slot order (any-hit connection rays),
 // 1 = near-first by a sorting network (closest-hit queries).
@@ -409,7 +399,7 @@ BDPT_HD int wave_count(bool p) {
 }
 // LM 3 (flat): tiny scenes test every leaf in order, no node fetches, no stack, no divergence
 // in the traversal loop (same hits and tie rule as a tree walk, bdpt_scene.cpp leaf_refs).
-BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? BDPT_LDS_BVH_WIDTH : BDPT_BVH_WIDTH; }
+BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? kLdsBvhWidth : kBvhWidth; }
 BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
 BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
@@ -662,7 +652,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   h.prim = -1;
   h.key = -1;
   h.b1 = 0; h.b2 = 0;
-  int stack_mem[BDPT_STACK];
+  int stack_mem[kStackMax];
   TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.closest++;
@@ -781,7 +771,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
 template <int LM = 0, int K = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
   RayInv r = make_rayinv(o, d);
-  int stack_mem[BDPT_STACK];
+  int stack_mem[kStackMax];
   TravStack<K> stk(stack_mem);
   int ref = S.root;
   c.shadow++;
@@ -1627,7 +1617,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
 #endif
-    bool end = !trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, rmin, rmax, h, cnt);
+    bool end = !trace_closest<LM, kWalkStack>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
     cnt.clk_walk_trace += tq1 - tq0;
@@ -2005,7 +1995,7 @@ BDPT_HD f3 pt_direct(const SceneView& S, const PtParams& pp, Rng& g, const Frame
       const f3 f = sample_f(M, g, w_out, &wi, &pdf);
       const f3 wiw = normalize(to_world(fr, wi));
       Hit h;
-      if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h, cnt)) continue;
+      if (!trace_closest<LM, kWalkStack>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h, cnt)) continue;
       f3 hn;
       int hm;
       shade_hit<LM>(S, h, hit_p, wiw, &hn, &hm);
@@ -2023,7 +2013,7 @@ BDPT_HD f3 pt_direct(const SceneView& S, const PtParams& pp, Rng& g, const Frame
       float dist, pdf;
       const f3 Le = light_sample_L(S, L, g, hit_p, &wiw, &dist, &pdf);
       const f3 f = bsdf_f_pt(M, w_out, to_local(fr, wiw));
-      if (trace_any<LM, BDPT_CONN_STACK>(S, hit_p, wiw, BDPT_EPS_F, dist - BDPT_EPS_F, cnt)) continue;
+      if (trace_any<LM, kConnStack>(S, hit_p, wiw, BDPT_EPS_F, dist - BDPT_EPS_F, cnt)) continue;
       const float ct = fabsf(dot(wiw, n));
       const f3 L_in = dist >= INFINITY ? Le : divs(Le, dist * dist);
       L_o = add(L_o, divs(muls(mul(L_in, f), ct), pdf));
@@ -2056,7 +2046,7 @@ BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int 
   f3 ro = add(mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]),
               add(add(smul(pLens.x, c0), smul(pLens.y, c1)), smul(pLens.z, c2)));
   Hit h;
-  if (!trace_closest<LM, BDPT_WALK_STACK>(S, ro, rd, S.cam.nclip, S.cam.fclip, h, cnt))
+  if (!trace_closest<LM, kWalkStack>(S, ro, rd, S.cam.nclip, S.cam.fclip, h, cnt))
     return S.env.light >= 0 ? env_radiance(S.env, rd) : splat3(0);
   f3 n;
   int mat;
@@ -2086,7 +2076,7 @@ BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int 
     const f3 f = sample_f(M, g, w_out, &wi, &pdf);
     const f3 wiw = normalize(to_world(fr, wi));
     Hit h2;
-    if (!trace_closest<LM, BDPT_WALK_STACK>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h2, cnt)) break;
+    if (!trace_closest<LM, kWalkStack>(S, hit_p, wiw, BDPT_EPS_F, INFINITY, h2, cnt)) break;
     f3 n2;
     int m2;
     shade_hit<LM>(S, h2, hit_p, wiw, &n2, &m2);

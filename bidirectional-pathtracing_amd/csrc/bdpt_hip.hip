@@ -99,7 +99,7 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
     const float tmax = q.tmax[k];
     vx = q.vx[k]; vy = q.vy[k]; vz = q.vz[k];
     tgt = q.tgt[k];
-    vis = !trace_any<LM, BDPT_CONN_STACK>(S, o, d, BDPT_EPS_F, tmax, cnt);
+    vis = !trace_any<LM, kConnStack>(S, o, d, BDPT_EPS_F, tmax, cnt);
   }
   if (vis && tgt < 0) {
     const int ow = ~tgt;
@@ -141,23 +141,17 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
 // mbcnt compaction) into the wave's LDS ring, and whenever 64 are queued the whole wave traces
 // them together — all 64 lanes busy on shadow rays regardless of per-lane path lengths.
-#ifndef BDPT_MIN_WAVES
-#define BDPT_MIN_WAVES 4   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
-#endif
-#ifndef BDPT_BLOCK
-#define BDPT_BLOCK 1024   // one block per CU: one LDS scene copy shared by its 16 waves
-#endif
-constexpr int kWavesPerBlock = BDPT_BLOCK / 64;
+constexpr int kMinWaves = 4;   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
+constexpr int kBlock = 1024;   // one block per CU: one LDS scene copy shared by its 16 waves
+constexpr int kWavesPerBlock = kBlock / 64;
 
 // Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
 // wave-uniform max|E| x max|L| grid (the special strategies stay wave-uniform). 0 = never, 1 =
 // always, 2 = for the long-path kernels (MAXV >= 8, m > 5), where the grid is mostly empty: measured
 // C5-shaped (m8, env, RR) 446 -> 470, CBgems m7 +0.9%; the m5 north star -1.7% (so grid there).
-#ifndef BDPT_CONN_COMPACT
-#define BDPT_CONN_COMPACT 2
-#endif
+constexpr int kConnCompact = 2;
 template <int MAXV>
-constexpr bool conn_compact() { return BDPT_CONN_COMPACT == 1 || (BDPT_CONN_COMPACT == 2 && MAXV >= 8); }
+constexpr bool conn_compact() { return kConnCompact == 1 || (kConnCompact == 2 && MAXV >= 8); }
 // Materials and lights copied to LDS (static arrays) when they fit: per-lane material / light
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
 // (measured: C2 +3%, Lucy stand-in +1%, CBgems +1%)
@@ -406,7 +400,7 @@ __device__ __forceinline__ void flush_stats(const KParams& kp, int lane, unsigne
 // EXT: environment light and/or Russian roulette; EXT = false is the reference-only
 // path with no trace of either in the generated code.
 template <int MAXV, bool STATS, int LM, bool EXT>
-__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_bdpt_sample(KParams kp) {
+__global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
   // One dynamic LDS array: [wave queues][optional scene / treelet copy]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ DMat s_mats[kLdsMats];
@@ -502,7 +496,7 @@ struct PtKParams {
 };
 
 template <bool STATS, int LM>
-__global__ __launch_bounds__(BDPT_BLOCK, BDPT_MIN_WAVES) void k_pt(PtKParams kp) {
+__global__ __launch_bounds__(kBlock, kMinWaves) void k_pt(PtKParams kp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   if (LM != 0) {
@@ -590,10 +584,7 @@ __global__ void k_combine(const float* a, const float* b, float* out, long long 
 // budget admits (16 waves per CU), minus their wave queues.
 constexpr size_t kLdsPerCu = 160 * 1024;
 // scenes up to this many primitives use the flat leaf-list traversal (LM 3)
-#ifndef BDPT_FLAT_MAX_PRIMS
-#define BDPT_FLAT_MAX_PRIMS 24   // measured: CBspheres 488 -> 511 Msamples/s, CBspheres_lambertian +6%, CBempty -1%
-#endif
-constexpr int kFlatMaxPrims = BDPT_FLAT_MAX_PRIMS;
+constexpr int kFlatMaxPrims = 24;   // flat leaf list up to this many primitives; measured: CBspheres 488 -> 511 Msamples/s, CBspheres_lambertian +6%, CBempty -1%
 constexpr size_t kBlocksPerCu = 16 / kWavesPerBlock;
 constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256 - kStaticLds;
 
@@ -602,11 +593,11 @@ constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * size
 template <class K>
 int launch_persistent(Ctx* c, K kernel, size_t lds, const KParams& kp) {
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BDPT_BLOCK, lds));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds));
   if (per_cu <= 0) { g_err = "k_bdpt_sample cannot be resident (LDS/VGPR budget)"; return BDPT_E_DEVICE; }
   long long grid = std::min<long long>((long long)per_cu * c->ncu,
                                        ((long long)kp.nitems + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(BDPT_BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(kBlock), lds, c->stream, kp);
   HIPCHK(hipGetLastError());
   return BDPT_OK;
 }
@@ -652,10 +643,10 @@ int launch_maxv(Ctx* c, KParams& kp) {
 template <class K, class KP>
 int launch_persistent_pt(Ctx* c, K kernel, size_t lds, const KP& kp, long long items) {
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BDPT_BLOCK, lds));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds));
   if (per_cu <= 0) { g_err = "k_pt cannot be resident (LDS/VGPR budget)"; return BDPT_E_DEVICE; }
   long long grid = std::min<long long>((long long)per_cu * c->ncu, (items + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)std::max(1LL, grid)), dim3(BDPT_BLOCK), lds, c->stream, kp);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)std::max(1LL, grid)), dim3(kBlock), lds, c->stream, kp);
   HIPCHK(hipGetLastError());
   return BDPT_OK;
 }

@@ -513,7 +513,7 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
       }
     }
     B.depth = wdepth;
-    if ((W - 1) * (wdepth + 1) + 2 > BDPT_STACK) {
+    if ((W - 1) * (wdepth + 1) + 2 > kStackMax) {
       err = "BVH deeper than the traversal stack";
       return BDPT_E_UNSUPPORTED;
     }

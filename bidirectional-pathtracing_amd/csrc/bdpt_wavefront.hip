@@ -34,10 +34,8 @@ namespace {
 constexpr int kBlock = 256;           // gen / shade / cand / connect
 constexpr int kTraceBlock = 512;      // trace / shadow: one LDS scene copy per 8 waves
 constexpr size_t kTraceLds = 40 * 1024;
-#ifndef BDPT_REG_STACK
-#define BDPT_REG_STACK 8
-#endif
-constexpr int kRegStack = BDPT_REG_STACK;   // traversal stack entries held in VGPRs
+constexpr int kWfRegStack = 8;
+constexpr int kRegStack = kWfRegStack;   // traversal stack entries held in VGPRs
 
 // Queues are striped: NS sub-queues, each with its own counter on its own 128-B line and its
 // own region of cap_s entries. A producer wave working on input chunk c pushes into stripe
@@ -611,10 +609,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_shadow(WfParams p) {
 // chunk (64 entries) from its static share of the striped queue; lanes advance one leaf visit
 // at a time and the wave refills while it is less than 3/4 busy.
 constexpr int kPool = 128;
-#ifndef BDPT_REFILL_BELOW
-#define BDPT_REFILL_BELOW 48
-#endif
-constexpr int kRefillBelow = BDPT_REFILL_BELOW;
+constexpr int kWfRefillBelow = 48;
+constexpr int kRefillBelow = kWfRefillBelow;
 
 struct WavePool {
   int* ids;
@@ -669,7 +665,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_rf(WfParams p) {
   Hit h;
   h.t = 0; h.prim = -1; h.key = -1; h.b1 = 0; h.b2 = 0;
   int ref = 0;
-  int stack_mem[BDPT_STACK];
+  int stack_mem[kStackMax];
   TravStack<kRegStack> stk(stack_mem);
   for (;;) {
     pool.refill(qv, nw);
@@ -715,7 +711,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_shadow_rf(WfParams p) {
   float tmax = 0;
   RayInv r = make_rayinv(mk3(1, 1, 1), mk3(1, 1, 1));
   int ref = 0;
-  int stack_mem[BDPT_STACK];
+  int stack_mem[kStackMax];
   TravStack<kRegStack> stk(stack_mem);
   for (;;) {
     pool.refill(qv, nw);

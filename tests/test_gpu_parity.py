@@ -479,3 +479,27 @@ def test_standin_counters_match_cpu_replay(lds, monkeypatch):
           f"tris gpu {st.tri_tests} replay {tris} ({st.tri_tests / tris:.4f})")
     assert nodes <= st.node_visits <= SPEC_EXCESS * nodes
     assert tris <= st.tri_tests <= SPEC_EXCESS * tris
+
+
+@pytest.mark.parametrize("env", [{"BDPT_WF_REFILL": "0"}, {"BDPT_WF_REFILL": "3"}, {"BDPT_WF_SLOTS": "4096"}])
+def test_wavefront_switches(env, tmp_path):
+    """The wavefront pipeline's run-time switches (read once per process, so each case runs in a
+    child process): traversal without lane refill (0), refill for connection rays too with the
+    separate k_wf_resolve (3), and a 4096-slot batch that splits the frame into many batches."""
+    import os
+    import subprocess
+    import sys
+    from _util import REPO
+    W, H, S, M = 96, 72, 2, 5
+    out = tmp_path / "wf.npy"
+    code = (f"import sys; sys.path[:0] = [{os.path.join(REPO, 'bidirectional-pathtracing_amd')!r}, "
+            f"{os.path.join(REPO, 'tests')!r}]\n"
+            "import numpy as np, bdpt_amd as B\nfrom _util import golden_scene\n"
+            f"sc = golden_scene('CBspheres', {W}, {H})\n"
+            f"pt = B.BidirectionalPathTracer(sc, {W}, {H}, {S}, {M}, pipeline=B.PIPELINE_WAVEFRONT)\n"
+            f"pt.raytrace_tiles()\nnp.save({str(out)!r}, pt.read_frame(B.FRAME_SAMPLE).astype(np.float64))\npt.close()\n")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    ref = oracle_render(golden_scene("CBspheres", W, H), W, H, S, M, MODE_C32)[0]
+    assert _rmse(np.load(out), ref) < RMSE_TOL
