@@ -196,7 +196,7 @@ def load_traffic(workload: str, kernel_ms: float):
     gbps = b / (kernel_ms * 1e-3) / 1e9
     pms = rec.get("kernel_ms")
     info = {"source": os.path.relpath(path, REPO), "read_bytes": rec.get("hbm_read_bytes"),
-            "write_bytes": rec.get("hbm_write_bytes"), "read_bytes_x2_upper": rec.get("hbm_read_bytes_x2_upper"),
+            "write_bytes": rec.get("hbm_write_bytes"),
             "gbps_at_this_kernel_ms": round(gbps, 2), "frac_at_this_kernel_ms": round(gbps / HBM_PEAK_GBPS, 5),
             "pmc_kernel_ms": pms}
     if pms:   # the bytes over the duration of the dispatch they were counted on (same rocprofv3 run)
@@ -405,8 +405,9 @@ def main() -> int:
                              "4-wide node, 32 B/child of a 2-wide one, 48 B/primitive record, 48 B/shading "
                              "record); gmem_* = the §8d bytes minus the scene reads served from the CU's LDS "
                              "copy (the part that goes through L2 / HBM); traffic = measured HBM-side bytes "
-                             "(PMC FETCH_SIZE + WRITE_SIZE, traffic_pmc.pmc_frac over the dispatch they were "
-                             "counted on)",
+                             "(PMC: 2 x FETCH_SIZE + WRITE_SIZE, FETCH_SIZE counting half the bytes of every "
+                             "read width this kernel uses, tools/fetch_calib.hip; traffic_pmc.pmc_frac over the "
+                             "dispatch they were counted on)",
                      "fetched_bytes_per_launch": fetched_launch,
                      "frac_fetched_bytes": round(fetched_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
                      "gmem_bytes_per_launch": gmem_launch,

@@ -4,9 +4,10 @@
 bench-sized launch of the workload (tools/prof_render.py), and that dispatch's duration from the
 kernel trace collected in the same rocprofv3 run (--pmc with --kernel-trace), so the bytes are tied
 to a measured kernel time. FETCH_SIZE / WRITE_SIZE are in KB (MI355X_MICROARCH.md, HBM section).
-The guide's x2 FETCH correction is calibrated for 16-B/lane streaming reads only; this kernel's
-memory-side reads are gathers (BVH nodes, primitives), scratch (path vertices, spilled registers)
-and frame atomics, so the raw value is reported as traffic and the x2 figure as an upper bound.
+FETCH_SIZE counts half of the bytes a read moves for every access width this kernel uses — 16-B
+and 4-B lane-interleaved streams, 16-B gathers at random lines (64 B per 128-B line) — and
+WRITE_SIZE counts 4-B stores exactly (tools/fetch_calib.hip, profiles/r03_fetch_calibration.log),
+so the HBM-side bytes of a launch are 2 x FETCH_SIZE + WRITE_SIZE.
 usage: pmc_traffic.py OUT_DIR WORKLOAD_KEY "description" """
 import csv
 import glob
@@ -48,14 +49,13 @@ def main():
         "workload_key": key,
         "kernel": fetch[1],
         "fetch_kb": fetch[0], "write_kb": write[0],
-        "hbm_read_bytes": fetch[0] * 1024, "hbm_write_bytes": write[0] * 1024,
-        "hbm_bytes_per_launch": (fetch[0] + write[0]) * 1024,
-        "hbm_read_bytes_x2_upper": 2 * fetch[0] * 1024,
+        "hbm_read_bytes": 2 * fetch[0] * 1024, "hbm_write_bytes": write[0] * 1024,
+        "hbm_bytes_per_launch": (2 * fetch[0] + write[0]) * 1024,
         "fetch_pass_kernel_ms": fms, "write_pass_kernel_ms": wms,
         "kernel_ms": (fms + wms) / 2 if fms and wms else None,
         "note": "FETCH_SIZE/WRITE_SIZE in KB, one launch, separate --pmc passes each with its own kernel "
-                "trace (kernel_ms = mean of the two dispatch durations); x2 FETCH correction (16-B "
-                "streaming reads) not applied",
+                "trace (kernel_ms = mean of the two dispatch durations); read bytes = 2 x FETCH_SIZE "
+                "(calibrated: profiles/r03_fetch_calibration.log)",
     }
     path = os.path.join(out, f"traffic_{key}.json")   # copied into profiles/ after the session
     with open(path, "w") as f:
