@@ -1633,7 +1633,11 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.fwd = 1; v.gp = 1; v.cq = 0;
       // eye_constants of an env vertex: g = 1 toward it, the previous vertex's BSDF density of rd
       // times its roulette probability; no prefix (the j = 0 weight recomputes this step)
-      if (count > 0) v.fwd = pdf_b(S.mats[pv_mat], prev_n, zaxis(prev_n), rd) * pv_q * 1.0f;
+      if (count > 0) {
+        const f3 pn = EXT ? P.E[count - 1].n : prev_n;
+        const int pm = EXT ? P.E[count - 1].mat : pv_mat;
+        v.fwd = pdf_b(S.mats[pm], pn, zaxis(pn), rd) * pv_q * 1.0f;
+      }
       v.gp = 0.0f;
       P.E[count++] = v;
     }
@@ -1662,24 +1666,38 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       // finished there: gp = horner(((pp * q) * g) / fwd_prev, t, gp_prev), cq = conn ? q : 0.
       const bool conn = M.type == MAT_DIFFUSE && lz(normalize(sub(ro, v.pos)), v.zh) >= 0 && nonzero3(v.alpha);
       const bool first_eye = !light && count == 1;
+      // the previous vertex. EXT kernels read it back from the path store (it was stored before
+      // this traversal) rather than hold it in registers across the traversal: C5 +1.5%; the
+      // reference-only kernels keep the registers (-0.3 .. -1.5% otherwise, profiles/r03_ab_pv_reload.log)
+      f3 pn = prev_n;
+      int pmat = pv_mat;
+      float pfwd = pv_fwd, pgp = pv_gp;
+      if (EXT) {
+        if (first_eye) {
+          pn = rd; pmat = -1; pfwd = 1.0f; pgp = 0.0f;
+        } else {
+          const Vtx& pvx = light ? P.L[count - 1] : P.E[count - 2];
+          pn = pvx.n; pmat = pvx.mat; pfwd = pvx.fwd; pgp = pvx.gp;
+        }
+      }
       float gp_pp = 0.0f, gp_g = 0.0f;
       if (first_eye) {
         v.fwd = 1.0f * 1.0f;
       } else {
         const bool nx_env = EXT && light && count == 1 && l1env;
-        const f3 nx_zh = nx_env ? prev_n : zaxis(prev_n);
+        const f3 nx_zh = nx_env ? pn : zaxis(pn);
         f3 dw;
         const float g2 = EXT ? step_gx(v.pos, v.n, false, ro, nx_zh, nx_env, &dw) : step_g(v.pos, v.n, ro, nx_zh, &dw);
         const float p = (light && count == 1) ? P.l1_dir_pdf
-                                              : pdf_b(S.mats[pv_mat], prev_n, nx_zh, dw) * (EXT ? pv_q : 1.0f);
+                                              : pdf_b(S.mats[pmat], pn, nx_zh, dw) * (EXT ? pv_q : 1.0f);
         v.fwd = p * g2;
-        gp_g = EXT ? step_gx(ro, prev_n, nx_env, v.pos, v.zh, false, &dw) : step_g(ro, prev_n, v.pos, v.zh, &dw);
+        gp_g = EXT ? step_gx(ro, pn, nx_env, v.pos, v.zh, false, &dw) : step_g(ro, pn, v.pos, v.zh, &dw);
         gp_pp = pdf_b(M, v.n, v.zh, dw);
       }
       const bool gp_t = !((dm >> (i - 2)) & 3u);
       auto finish = [&](float q) {   // q: this vertex's roulette probability (1 without roulette)
         v.cq = conn ? (EXT ? q : 1.0f) : 0.0f;
-        v.gp = first_eye ? 0.0f : mis_horner(((EXT ? gp_pp * q : gp_pp) * gp_g) / pv_fwd, gp_t, pv_gp);
+        v.gp = first_eye ? 0.0f : mis_horner(((EXT ? gp_pp * q : gp_pp) * gp_g) / pfwd, gp_t, pgp);
         pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp; pv_q = q;
       };
       if (!EXT) finish(1.0f);
