@@ -77,18 +77,25 @@ BDPT_HD f3 splat3(float c) { return mk3(c, c, c); }
 struct Frame {
   f3 X, Y, Z;
 };
-BDPT_HD Frame make_frame(f3 n) {
+template <bool UNIT = false>
+BDPT_HD Frame make_frame_t(f3 n) {
   f3 z = n, h = n;
   if (fabsf(h.x) <= fabsf(h.y) && fabsf(h.x) <= fabsf(h.z)) h.x = 1.0f;
   else if (fabsf(h.y) <= fabsf(h.x) && fabsf(h.y) <= fabsf(h.z)) h.y = 1.0f;
   else h.z = 1.0f;
-  z = normalize(z);
+  if (!UNIT) z = normalize(z);
   f3 y = normalize(cross(h, z));
   f3 x = normalize(cross(z, y));
   Frame f;
   f.X = x; f.Y = y; f.Z = z;
   return f;
 }
+BDPT_HD Frame make_frame(f3 n) { return make_frame_t<false>(n); }
+// The frame of a surface hit. Its shading normal is already normalize()d (shade_hit), so the
+// fp32 semantics take Z = n instead of normalising it a second time (which moves a component by
+// at most an ulp, in about 1 of 4 normals): one normalize less per vertex, and a stored path
+// vertex needs no separate shading axis (oracle mode 2 does the same).
+BDPT_HD Frame make_frame_hit(f3 n) { return make_frame_t<true>(n); }
 // o2w * v (matrix3x3.cpp:110-114) and w2o * v = o2w.T() * v
 BDPT_HD f3 to_world(const Frame& f, f3 v) { return add(add(smul(v.x, f.X), smul(v.y, f.Y)), smul(v.z, f.Z)); }
 BDPT_HD float lz(f3 v, f3 Z) { return v.x * Z.x + v.y * Z.y + v.z * Z.z; }   // (w2o*v).z
@@ -1104,7 +1111,7 @@ BDPT_HD float pdf_b(const DMat& M, f3 n, f3 zh, f3 dw) {
     case MAT_MIRROR:
     case MAT_REFRACTION: return 1.0f;
     default: {
-      Frame f = make_frame(n);
+      Frame f = make_frame_hit(n);
       f3 wi = to_local(f, dw), wt;
       if (!refract_dir(wi, &wt, M.ior)) return 1.0f;
       float c = fabsf(wt.z) / norm(wt);
@@ -1241,10 +1248,42 @@ struct LightSample {
   bool env;    // environment light: n = zh = -w, pos unused
 };
 
+// A vertex as the path store holds it: the shading axis zh is not stored (it is zaxis(n), or n
+// itself for an environment vertex, and is recomputed where a connection reads it), and in the
+// reference-only kernels (EXT = false) the connectability flag rides in bit 16 of the material
+// word, so a vertex is 12 dwords (48 B) instead of 16; EXT kernels keep cq (the roulette
+// probability of a connectable vertex) as a 13th dword. The private segment is lane-interleaved
+// per dword, so the dwords a kernel never touches cost no traffic.
+struct VtxS {
+  f3 pos;
+  float fwd;
+  f3 n;
+  float gp;
+  f3 alpha;
+  int mb;     // material id (low 16 bits, signed); EXT = false: bit 16 = can_connect
+  float cq;   // EXT only
+};
+BDPT_HD int vs_mat(const VtxS& s) { return (int)(short)(s.mb & 0xffff); }
+template <bool EXT>
+BDPT_HD void vtx_store(VtxS& s, const Vtx& v) {
+  s.pos = v.pos; s.fwd = v.fwd; s.n = v.n; s.gp = v.gp; s.alpha = v.alpha;
+  s.mb = (v.mat & 0xffff) | (!EXT && v.cq > 0.0f ? 0x10000 : 0);
+  if (EXT) s.cq = v.cq;
+}
+template <bool EXT>
+BDPT_HD Vtx vtx_load(const VtxS& s) {
+  Vtx v;
+  v.pos = s.pos; v.fwd = s.fwd; v.n = s.n; v.gp = s.gp; v.alpha = s.alpha;
+  v.mat = vs_mat(s);
+  v.cq = EXT ? s.cq : ((s.mb >> 16) != 0 ? 1.0f : 0.0f);
+  v.zh = v.n;   // hit vertices: make_frame_hit; environment vertices: n = zh = -w; L[1]'s zh is never read
+  return v;
+}
+
 template <int MAXV>
 struct Paths {
-  Vtx E[MAXV];       // E[k] at index k-2 (k >= 2): eye hits
-  Vtx L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
+  VtxS E[MAXV];       // E[k] at index k-2 (k >= 2): eye hits
+  VtxS L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
   uint32_t dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
   float l1_dir_pdf;
@@ -1481,13 +1520,13 @@ BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const V
 }
 
 // Path accessor over one lane's Paths (megakernel, host tests).
-template <int MAXV>
+template <int MAXV, bool EXT>
 struct PathsInRegs {
   const Paths<MAXV>& P;
   uint32_t dE, dL;
   BDPT_HD explicit PathsInRegs(const Paths<MAXV>& p) : P(p), dE(p.dE), dL(p.dL) {}
-  BDPT_HD Vtx e(int k) const { return P.E[k - 2]; }
-  BDPT_HD Vtx l(int k) const { return P.L[k - 1]; }
+  BDPT_HD Vtx e(int k) const { return vtx_load<EXT>(P.E[k - 2]); }
+  BDPT_HD Vtx l(int k) const { return vtx_load<EXT>(P.L[k - 1]); }
 };
 
 // Eye and light subpaths of one pixel-sample plus their MIS constants
@@ -1574,7 +1613,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     lpp = lpp / (float)S.nlights;
     mis_p = mis_p / (float)S.nlights;
     alpha1 = divs(lrad, lpp);
-    Vtx& v1 = P.L[0];
+    Vtx v1;
     v1.pos = lo;
     v1.n = ln;
     v1.zh = l1env ? ln : zaxis(ln);
@@ -1582,6 +1621,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
     v1.mat = l1env ? (int)MAT_ENV_V : -1;
     v1.gp = 0; v1.cq = 0;
     v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused walk)
+    vtx_store<EXT>(P.L[0], v1);
     P.l1_dir_pdf = mis_dir;
   };
   Rng gl0 = g;
@@ -1635,18 +1675,18 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       // times its roulette probability; no prefix (the j = 0 weight recomputes this step)
       if (count > 0) {
         const f3 pn = EXT ? P.E[count - 1].n : prev_n;
-        const int pm = EXT ? P.E[count - 1].mat : pv_mat;
-        v.fwd = pdf_b(S.mats[pm], pn, zaxis(pn), rd) * pv_q * 1.0f;
+        const int pm = EXT ? vs_mat(P.E[count - 1]) : pv_mat;
+        v.fwd = pdf_b(S.mats[pm], pn, pn, rd) * pv_q * 1.0f;
       }
       v.gp = 0.0f;
-      P.E[count++] = v;
+      vtx_store<EXT>(P.E[count++], v);
     }
     if (!end) {
       f3 n;
       int mat;
       shade_hit<LM>(S, h, ro, rd, &n, &mat);
       const DMat M = S.mats[mat];
-      const Frame fr = make_frame(n);
+      const Frame fr = make_frame_hit(n);
       const f3 hit_p = add(ro, muls(rd, h.t));
       Vtx v;
       v.alpha = nalpha;
@@ -1655,7 +1695,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       v.zh = fr.Z;
       v.mat = mat;
       v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
-      Vtx* slot = (light ? P.L + 1 : P.E) + count++;
+      VtxS* slot = (light ? P.L + 1 : P.E) + count++;
       if (is_delta(M.type)) dm |= 1u << i;
       // eye_constants / light_constants of this vertex at its creation. The previous vertex is the
       // one just below it on the same subpath (camera: no step; the light vertex L[1] for the
@@ -1676,8 +1716,8 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         if (first_eye) {
           pn = rd; pmat = -1; pfwd = 1.0f; pgp = 0.0f;
         } else {
-          const Vtx& pvx = light ? P.L[count - 1] : P.E[count - 2];
-          pn = pvx.n; pmat = pvx.mat; pfwd = pvx.fwd; pgp = pvx.gp;
+          const VtxS& pvx = light ? P.L[count - 1] : P.E[count - 2];
+          pn = pvx.n; pmat = vs_mat(pvx); pfwd = pvx.fwd; pgp = pvx.gp;
         }
       }
       float gp_pp = 0.0f, gp_g = 0.0f;
@@ -1685,7 +1725,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         v.fwd = 1.0f * 1.0f;
       } else {
         const bool nx_env = EXT && light && count == 1 && l1env;
-        const f3 nx_zh = nx_env ? pn : zaxis(pn);
+        // the previous vertex's shading axis: a surface hit's is its normal (make_frame_hit), the
+        // light vertex L[1]'s is zaxis(n) (an environment L[1] keeps n)
+        const f3 nx_zh = (nx_env || !(light && count == 1)) ? pn : zaxis(pn);
         f3 dw;
         const float g2 = EXT ? step_gx(v.pos, v.n, false, ro, nx_zh, nx_env, &dw) : step_g(v.pos, v.n, ro, nx_zh, &dw);
         const float p = (light && count == 1) ? P.l1_dir_pdf
@@ -1701,7 +1743,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
         pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp; pv_q = q;
       };
       if (!EXT) finish(1.0f);
-      *slot = v;
+      vtx_store<EXT>(*slot, v);
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
         if (EXT) {
@@ -1759,7 +1801,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       ro = P.L[0].pos; rd = P.l1_d; prev_n = P.L[0].n;
       nalpha = next_alpha(P.L[0].alpha, prev_n, rd, splat3(1.0f), P.l1_pdf);
       mis_p = P.L[0].fwd;
-      l1env = P.L[0].mat == (int)MAT_ENV_V;
+      l1env = vs_mat(P.L[0]) == (int)MAT_ENV_V;
       rmin = BDPT_EPS_F; rmax = INFINITY;
       i = 2; count = 0; dm = 0;
       pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
@@ -1913,7 +1955,7 @@ BDPT_HD f3 render_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>
   for (int i = 1; i < P.nE; i++) {
     for (int j = 0; j < P.nL; j++) {
       Conn cn;
-      int kind = make_conn<EXT>(S, sp, PathsInRegs<MAXV>(P), g, i, j, cn);
+      int kind = make_conn<EXT>(S, sp, PathsInRegs<MAXV, EXT>(P), g, i, j, cn);
       if (kind == CONN_DIRECT) {
         eye_sum = add(eye_sum, cn.val);
       } else if (kind == CONN_RAY) {
@@ -2079,7 +2121,7 @@ BDPT_HD f3 pt_sample(const SceneView& S, const PtParams& pp, Counters& cnt, int 
   int k = 0;
   for (;; k++) {
     const DMat M = S.mats[mat];
-    const Frame fr = make_frame(n);
+    const Frame fr = make_frame_hit(n);
     const f3 hit_p = add(ro, muls(rd, h.t));
     const f3 w_out = to_local(fr, neg(rd));
     const bool dl = is_delta(M.type);

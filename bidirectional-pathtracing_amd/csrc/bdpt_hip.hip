@@ -449,7 +449,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
       ph_cells += (unsigned)(max(wave_max(nE) - 1, 0) * wave_max(nL));
       ph_pairs += (unsigned)(max(nE - 1, 0) * nL);
 #endif
-      connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV>(P), g, nE, nL, lane, inv, cs, cnt);
+      connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV, EXT>(P), g, nE, nL, lane, inv, cs, cnt);
     }
     finish_item<LM>(kp, q, it, lane, cs, cnt);
 #ifdef BDPT_PHASE_PROF

@@ -197,7 +197,7 @@ struct PathsStore {
     r.fwd = a.w;
     r.n = mk3(b.x, b.y, b.z);
     r.gp = b.w;
-    r.zh = zaxis(r.n);
+    r.zh = r.n;   // make_frame_hit (bdpt_core.h); L[1]'s zh is never read
     r.alpha = mk3(c.x, c.y, c.z);
     const unsigned bits = __float_as_uint(c.w);
     r.mat = (int)(short)(bits & 0xffffu);
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(WfParams p) {
         int mat;
         shade_hit(S, h, ro, rd, &nrm, &mat);
         const DMat M = S.mats[mat];
-        const Frame fr = make_frame(nrm);
+        const Frame fr = make_frame_hit(nrm);
         const f3 hit_p = add(ro, muls(rd, h.t));
         const float cp = dot(prev_n, rd);
         const f3 alpha = divs(mul(muls(prev_alpha, fabsf(cp)), prev_f), prev_pdf);
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(WfParams p) {
         const int conn = M.type == MAT_DIFFUSE && lz(normalize(sub(ro, hit_p)), zh) >= 0 && nonzero3(alpha);
         float fwd = 1.0f * 1.0f, gp = 0.0f;
         if (kind != 0 || i > 2) {
-          const f3 pzh = zaxis(prev_n);
+          const f3 pzh = (kind != 0 && i == 2) ? zaxis(prev_n) : prev_n;   // L[1] / a hit (make_frame_hit)
           f3 dw;
           const float g2 = step_g(hit_p, nrm, ro, pzh, &dw);
           const float pf = (kind != 0 && i == 2) ? a3.w : pdf_b(S.mats[__float_as_int(a3.z)], prev_n, pzh, dw) * 1.0f;

@@ -21,6 +21,7 @@
 // vector3D.h) so that mode 0 reproduces the reference's fp64 bits. Build: -O2 -ffp-contract=off.
 
 #include <cmath>
+#include <type_traits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -97,6 +98,28 @@ Frame<R> make_coord_space(const V3<R>& n) {
   else
     h.z = 1.0;
   z.normalize();
+  V3<R> y = cross(h, z);
+  y.normalize();
+  V3<R> x = cross(z, y);
+  x.normalize();
+  return Frame<R>{x, y, z};
+}
+
+// The frame of a surface hit (isect.mat >= 0). Mode 2 restates the device's fp32 semantics,
+// which take Z = n for a hit normal (already unit length: the intersection normalises it) instead
+// of normalising it again (bdpt_core.h make_frame_hit); modes 0 and 1 (fp64) keep
+// the reference's make_coord_space, so mode 0 stays bit-exact with the reference.
+template <class R>
+Frame<R> hit_coord_space(const V3<R>& n) {
+  if (!std::is_same<R, float>::value) return make_coord_space(n);
+  V3<R> z(n.x, n.y, n.z);
+  V3<R> h = z;
+  if (std::fabs(h.x) <= std::fabs(h.y) && std::fabs(h.x) <= std::fabs(h.z))
+    h.x = 1.0;
+  else if (std::fabs(h.y) <= std::fabs(h.x) && std::fabs(h.y) <= std::fabs(h.z))
+    h.y = 1.0;
+  else
+    h.z = 1.0;
   V3<R> y = cross(h, z);
   y.normalize();
   V3<R> x = cross(z, y);
@@ -1323,7 +1346,7 @@ struct Tracer {
         break;
       }
       r.max_t = isect.t;  // (not read again: the next ray is rebuilt below)
-      Frame<R> f = make_coord_space(isect.n);
+      Frame<R> f = hit_coord_space(isect.n);
       const V hit_p = r.o + r.d * isect.t;
       const V w_out = f.to_local(-r.d);
       V wi, fv, wi_world;
@@ -1379,7 +1402,7 @@ struct Tracer {
   R step(const Vertex& cur, const Vertex& oth, V* d_out) const {
     if (cur.env) { *d_out = -cur.isect.n; return R(1.); }
     if (oth.env) { *d_out = oth.isect.n; return std::fabs(dot(oth.isect.n, cur.isect.n)); }
-    Frame<R> f = make_coord_space(oth.isect.n);
+    Frame<R> f = oth.isect.mat >= 0 ? hit_coord_space(oth.isect.n) : make_coord_space(oth.isect.n);
     V wi_world = cur.position - oth.position;
     R dist = wi_world.norm();
     wi_world.normalize();
@@ -1389,7 +1412,7 @@ struct Tracer {
   }
   R pdf_from(const Vertex& v, const V& d) const {   // v.bsdf->sample_pdf(0, frame(v.n)^T d)
     V wo;
-    return bsdf_sample_pdf(v.isect.mat, wo, make_coord_space(v.isect.n).to_local(d));
+    return bsdf_sample_pdf(v.isect.mat, wo, hit_coord_space(v.isect.n).to_local(d));
   }
 
   R mis_weight(int i_eye, int i_light, const std::vector<Vertex>& E, const std::vector<Vertex>& L,
@@ -1501,7 +1524,7 @@ struct Tracer {
   int ns_area_light = 1;
   bool hemisphere = false;   // direct_hemisphere_sample (-H)
   V pt_direct_hemisphere(const Ray<R>& r, const Isect& isect) {              // :47-97
-    Frame<R> o2w = make_coord_space(isect.n);
+    Frame<R> o2w = hit_coord_space(isect.n);
     const V hit_p = r.o + r.d * isect.t;
     const V w_out = o2w.to_local(-r.d);
     int num_samples = (int)sc.lights.size() * ns_area_light;
@@ -1524,7 +1547,7 @@ struct Tracer {
     return L_out;
   }
   V pt_direct_importance(const Ray<R>& r, const Isect& isect) {              // :99-169
-    Frame<R> o2w = make_coord_space(isect.n);
+    Frame<R> o2w = hit_coord_space(isect.n);
     const V hit_p = r.o + r.d * isect.t;
     const V w_out = o2w.to_local(-r.d);
     V L_out;
@@ -1550,7 +1573,7 @@ struct Tracer {
     return L_out;
   }
   V pt_at_least_one_bounce(const Ray<R>& r, int depth, const Isect& isect) {   // :181-262
-    Frame<R> o2w = make_coord_space(isect.n);
+    Frame<R> o2w = hit_coord_space(isect.n);
     V hit_p = r.o + r.d * isect.t;
     V w_out = o2w.to_local(-r.d);
     V L_out, L_o;
@@ -1675,7 +1698,7 @@ struct Tracer {
         ve = ES;
       }
       if (i_eye > 1) {
-        Frame<R> f = make_coord_space(E[i_eye].isect.n);
+        Frame<R> f = hit_coord_space(E[i_eye].isect.n);
         V er = E[i_eye - 1].position - E[i_eye].position;
         er.normalize();
         er = f.to_local(er);
@@ -1689,7 +1712,7 @@ struct Tracer {
         f_eye = bsdf_f(E[i_eye].isect.mat, er, connect);
       }
       if (i_light > 1) {
-        Frame<R> f = make_coord_space(L[i_light].isect.n);
+        Frame<R> f = hit_coord_space(L[i_light].isect.n);
         V lr = L[i_light - 1].position - L[i_light].position;
         lr.normalize();
         lr = f.to_local(lr);
