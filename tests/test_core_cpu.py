@@ -133,3 +133,17 @@ def test_device_pipeline_bit_exact_mesh_trees(scene, W, H, spp, M):
     assert np.isfinite(eye).all() and np.isfinite(light).all()
     assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
     assert np.array_equal(light, olight), f"light max diff {np.abs(light - olight).max()}"
+
+
+def test_triangle_early_outs_exact(tmp_path):
+    """tri_test's division-free early-outs (b1 + b2 certainly > 1, t certainly > tmax) decide
+    exactly as the plain three-division Möller–Trumbore predicate (triangle.cpp:57-95) on 1M random
+    and near-boundary cases (tests/native/tri_exact.cpp)."""
+    import subprocess
+    exe = str(tmp_path / "tri_exact")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I" + os.path.join(REPO, "include"),
+                    "-I" + os.path.join(REPO, "bidirectional-pathtracing_amd", "csrc"), "-o", exe,
+                    os.path.join(REPO, "tests", "native", "tri_exact.cpp")], check=True)
+    out = subprocess.run([exe, "1000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "mismatches 0" in out.stdout
