@@ -319,19 +319,6 @@ BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f
   if (quot_neg(n2, denom) || quot_gt1(n2, denom)) return false;
   float nt = dot(s2, e2);
   if (tmin >= 0 && quot_neg(nt, denom)) return false;
-  // Two more exact early-outs, for |denom| and |denom| * tmax in the normal range (>= 2^-100):
-  // (1) b1 + b2 > 1 certainly: n1, n2 carry denom's sign (or are below 2^-60 of it), so
-  //     |n1 + n2| >= fl(|denom| (1 + 2^-20)) gives q1 + q2 >= 1 + 2^-21 exactly, and then the
-  //     rounded b1, b2 (each off by <= 2^-24 of a value <= 1) sum to > 1 + 2^-23;
-  // (2) t > tmax certainly: |nt| > fl(fl(|denom| tmax) (1 + 2^-19)) gives nt / denom >
-  //     tmax (1 + 2^-20), whose rounding is > tmax (tmax = inf never takes it; with tmin >= 0 a
-  //     certainly negative t has already left, so nt carries denom's sign).
-  const float ad = fabsf(denom);
-  if (ad >= 7.88860905e-31f) {   // 2^-100
-    if (fabsf(n1 + n2) >= ad * 1.00000095367431640625f) return false;
-    const float adt = ad * tmax;
-    if (tmin >= 0 && adt >= 7.88860905e-31f && fabsf(nt) > adt * 1.0000019073486328125f) return false;
-  }
   float t = nt / denom;
   float b1 = n1 / denom;
   float b2 = n2 / denom;
@@ -423,15 +410,6 @@ BDPT_HD constexpr int lm_width(int LM) { return LM == 1 || LM == 3 ? kLdsBvhWidt
 BDPT_HD constexpr int node_f4(int W) { return W == 4 ? 8 : 4; }        // float4 per node (stride)
 BDPT_HD constexpr int node_used_f4(int W) { return W == 4 ? 7 : 4; }   // float4 a traversal reads
 BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
-// The LDS copy of a 4-wide node drops its 16-B pad (7 float4, 112 B): 14% more treelet nodes in
-// the same LDS. HBM keeps the 128-B stride (one cache line per node).
-#ifndef BDPT_LDS_NODE4
-#define BDPT_LDS_NODE4 7
-#endif
-BDPT_HD constexpr int lds_node_f4(int W) { return W == 4 ? BDPT_LDS_NODE4 : 4; }
-BDPT_HD constexpr int lds_node_bytes(int W) { return 16 * lds_node_f4(W); }
-// float4 k of the LDS node copy, read from the HBM node array (staging loops)
-BDPT_HD int lds_node_src(int W, int k) { return (k / lds_node_f4(W)) * node_f4(W) + k % lds_node_f4(W); }
 
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
 // ones in a private array (K = 0: all of it). Near-first traversal of these trees rarely holds more
@@ -577,7 +555,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
   float4 v[NU];
   if (LM == 1) {   // all nodes in LDS: plain ds_reads the compiler schedules
 #pragma unroll
-    for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + lds_node_f4(W) * ref + k);
+    for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
     c.lnodes += W;
   } else if (LM == 2) {
     // Treelet (LDS) and HBM lanes in one wave: a lane-divergent if / else over the same registers
@@ -592,7 +570,7 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     const bool all_lds = in_lds;
 #endif
     if (all_lds) {
-      ld_node_lds<W>(S.lnodes + lds_node_f4(W) * ref, v);
+      ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
       c.lnodes += W;
     } else {
 #pragma unroll

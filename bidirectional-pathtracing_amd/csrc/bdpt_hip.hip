@@ -171,10 +171,10 @@ template <int LM>
 __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DMat* s_mats, DLight* s_lights) {
   if (LM != 0) {
     float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
-    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : lds_node_f4(lm_width(LM)) * kp.S.ntop;
+    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
-      sc[k] = k < nn ? kp.S.nodes[lds_node_src(lm_width(LM), k)] : kp.S.geom[k - nn];
+      sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
     if (LM == 3) {
       int* lv = (int*)(sc + n4);
       for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
@@ -501,10 +501,9 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_pt(PtKParams kp) {
   const int lane = threadIdx.x & 63;
   if (LM != 0) {
     float4* sc = (float4*)smem;
-    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : lds_node_f4(lm_width(LM)) * kp.S.ntop;
+    const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
-    for (int k = threadIdx.x; k < n4; k += blockDim.x)
-      sc[k] = k < nn ? kp.S.nodes[lds_node_src(lm_width(LM), k)] : kp.S.geom[k - nn];
+    for (int k = threadIdx.x; k < n4; k += blockDim.x) sc[k] = k < nn ? kp.S.nodes[k] : kp.S.geom[k - nn];
     if (LM == 3) {
       int* lv = (int*)(sc + n4);
       for (int k = threadIdx.x; k < kp.S.nleaves; k += blockDim.x) lv[k] = kp.S.lleaves[k];
@@ -618,10 +617,10 @@ int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
   if (lm == 2 && !has_nodes) lm = 0;
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
-  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / lds_node_bytes(lm_width(2)));
+  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
   if (lm == 2 && c->env_ntop_max >= 0) kp.S.ntop = std::min(kp.S.ntop, c->env_ntop_max);   // diagnostics
   c->last_lm = lm;
-  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * lds_node_bytes(lm_width(2)) : 0);
+  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
   return lm;
 }
 
@@ -666,10 +665,10 @@ int launch_pt(Ctx* c, PtKParams& kp) {
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
-  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, lds_max / lds_node_bytes(lm_width(2)));
+  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, lds_max / node_bytes(lm_width(2)));
   if (lm == 3) return launch_persistent_pt(c, k_pt<STATS, 3>, flat, kp, kp.nblocks);
   if (lm == 1) return launch_persistent_pt(c, k_pt<STATS, 1>, full, kp, kp.nblocks);
-  if (lm == 2) return launch_persistent_pt(c, k_pt<STATS, 2>, (size_t)kp.S.ntop * lds_node_bytes(lm_width(2)), kp, kp.nblocks);
+  if (lm == 2) return launch_persistent_pt(c, k_pt<STATS, 2>, (size_t)kp.S.ntop * node_bytes(lm_width(2)), kp, kp.nblocks);
   return launch_persistent_pt(c, k_pt<STATS, 0>, 0, kp, kp.nblocks);
 }
 

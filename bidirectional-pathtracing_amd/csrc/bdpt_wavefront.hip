@@ -212,10 +212,9 @@ struct PathsStore {
 template <int LM>
 __device__ __forceinline__ void stage_scene(WfParams& p, float4* sc) {
   if (LM == 0) return;
-  const int nn = LM == 1 ? p.n_node4 : lds_node_f4(lm_width(LM)) * p.S.ntop;
+  const int nn = LM == 1 ? p.n_node4 : node_f4(lm_width(LM)) * p.S.ntop;
   const int n4 = nn + (LM == 1 ? p.n_geom4 : 0);
-  for (int k = threadIdx.x; k < n4; k += blockDim.x)
-    sc[k] = k < nn ? p.S.nodes[lds_node_src(lm_width(LM), k)] : p.S.geom[k - nn];
+  for (int k = threadIdx.x; k < n4; k += blockDim.x) sc[k] = k < nn ? p.S.nodes[k] : p.S.geom[k - nn];
   __syncthreads();
   p.S.lnodes = sc;
   p.S.lgeom = sc + nn;
@@ -847,10 +846,10 @@ int wf_alloc(Ctx* c) {
   w->lm = lenv ? atoi(lenv) : (full <= kTraceLds ? 1 : 2);
   if (w->lm == 1 && full > kTraceLds) w->lm = 2;
   if (w->lm == 2) {
-    w->ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kTraceLds / lds_node_bytes(lm_width(2)));
+    w->ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kTraceLds / node_bytes(lm_width(2)));
     if (w->ntop <= 0) w->lm = 0;
   }
-  w->lds = w->lm == 1 ? full : w->lm == 2 ? (size_t)w->ntop * lds_node_bytes(lm_width(2)) : 0;
+  w->lds = w->lm == 1 ? full : w->lm == 2 ? (size_t)w->ntop * node_bytes(lm_width(2)) : 0;
   return BDPT_OK;
 }
 

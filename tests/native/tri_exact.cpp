@@ -1,4 +1,4 @@
-// Test-only: bdpt::tri_test (with its exact early-outs) against the plain Möller–Trumbore
+// Test-only: bdpt::tri_test (with its exact quotient-sign / > 1 early-outs) against the plain Möller–Trumbore
 // predicate it must reproduce (three correctly rounded divisions, then the reference's
 // comparisons, triangle.cpp:57-95), on random and on near-boundary cases (b1 + b2 close to 1,
 // t close to tmax, tiny and huge denominators). Prints the number of mismatches.

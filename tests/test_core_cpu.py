@@ -136,9 +136,9 @@ def test_device_pipeline_bit_exact_mesh_trees(scene, W, H, spp, M):
 
 
 def test_triangle_early_outs_exact(tmp_path):
-    """tri_test's division-free early-outs (b1 + b2 certainly > 1, t certainly > tmax) decide
-    exactly as the plain three-division Möller–Trumbore predicate (triangle.cpp:57-95) on 1M random
-    and near-boundary cases (tests/native/tri_exact.cpp)."""
+    """tri_test with its division-free early-outs (a quotient certainly < 0 or > 1) decides, and
+    rounds t / b1 / b2, exactly as the plain three-division Möller–Trumbore predicate
+    (triangle.cpp:57-95) on 1M random and near-boundary cases (tests/native/tri_exact.cpp)."""
     import subprocess
     exe = str(tmp_path / "tri_exact")
     subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I" + os.path.join(REPO, "include"),
