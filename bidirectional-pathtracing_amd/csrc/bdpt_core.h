@@ -1547,9 +1547,9 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   const f3 cam = mk3(S.cam.pos[0], S.cam.pos[1], S.cam.pos[2]);
   f3 rd = camera_dir(S.cam, dx, dy);
   // sample_light_ray (bidirection.cpp:105-118), AreaLight/PointLight::sample_Le, on stream 1: the
-  // light vertex L[1] and the light walk's first ray. BDPT_LATE_LIGHT: drawn when the lane's eye
-  // walk ends instead of before it (same stream, same values), so the ~17 registers of the light
-  // sample are not live across the eye walk's traversals.
+  // light vertex L[1] and the light walk's first ray, drawn before the eye walk and kept in the path
+  // store (read back when the light walk starts), so the ~17 registers of the light sample are not
+  // live across the eye walk's traversals (drawing them at the switch instead spilled more).
   bool l1env = false;
   float mis_p = 0.0f;   // L[1]'s MIS point density (differs from lpp only for the env light)
   auto sample_light = [&](Rng& gl, f3& lo, f3& ld, f3& ln, f3& alpha1, float& ldp) {
