@@ -15,10 +15,12 @@ reference: a synthetic sky of the same role stands in, tools/envmap.py).
 Multi-GPU (torchrun, one rank per GPU), strong scaling by default: the step's fixed render (the
 workload's spp of every pixel) is split by sample range — rank r renders global sample indices
 [s*spp + r*spp/N, s*spp + (r+1)*spp/N) of step s (sample keys are global, so the image does not
-depend on N up to fp32 summation order) — and the W*H*3 fp32 frames are summed by one RCCL reduce
-onto rank 0 inside the timed region (splats land anywhere, so a tile gather would not do,
-SURVEY.md §8e). --scaling weak gives every rank the full spp instead. value = pixel-samples of all
-ranks / max-over-ranks wall time.
+depend on N up to fp32 summation order) — and the W*H*3 fp32 frames are summed by one all-reduce
+inside the timed region (splats land anywhere, so a tile gather would not do). The
+split and the reduce are the product's bdpt_amd.ShardedRender; --dist-backend picks RCCL ("nccl",
+the default) or gloo (the same all_reduce of the device tensor; two ranks can then share one GPU,
+--devices 0,0, as tests/test_gpu_multirank.py runs it). --scaling weak gives every rank the full
+spp instead. value = pixel-samples of all ranks / max-over-ranks wall time.
 """
 from __future__ import annotations
 
@@ -55,15 +57,7 @@ BYTES_NODE, BYTES_TRI, BYTES_SPH, BYTES_HIT = 32, 36, 16, 40
 BYTES_ENV_SAMPLE, BYTES_ENV_LOOKUP, BYTES_ENV_PDF = 76, 48, 4
 
 
-def rank_sample_range(step: int, rank: int, world: int, spp: int, scaling: str = "strong"):
-    """Global sample indices [begin, begin + count) that `rank` renders in `step`.
-    strong: the step's fixed render of `spp` samples per pixel is split across the ranks;
-    weak: every rank renders a fresh `spp` of its own. Either way every (step, rank) owns a
-    disjoint range, so the summed frames equal one render of all those samples."""
-    if scaling == "strong":
-        lo, hi = spp * rank // world, spp * (rank + 1) // world
-        return step * spp + lo, hi - lo
-    return (step * world + rank) * spp, spp
+from bdpt_amd import rank_sample_range  # noqa: E402  (the multi-GPU split lives in the product module)
 
 
 def algorithmic_bytes(st) -> int:
@@ -132,52 +126,99 @@ def cpu_baseline(scene, name: str, W: int, H: int, SPP: int, M: int, threads: in
 REF_DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
 
 
-def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads: int, budget_s: float = 15.0):
-    """The reference's own `-t N` CPU path: oracle/_ref/ref_driver (built by __graft_entry__.build()
-    from the reference's sources: RaytracedRenderer + BidirectionalPathTracer, reference flags)
-    rendering the same scene and resolution at a few spp. Render seconds are the reference's own
-    "Rendering... 100%! (Xs)" report (tiles + its per-tile frame tonemap, excluding parse/BVH
-    build). None when the binary is not present."""
+def host_cores() -> dict:
+    """The host CPUs this process may run on: nproc (os.cpu_count(), the whole node), the
+    affinity mask, and the cgroup CPU quota where one is set (a GPU box's share of its node).
+    `usable` = the smallest of them: the thread count the CPU baselines run at."""
+    n = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return {"nproc": n, "affinity": aff, "cgroup_quota": quota, "usable": min(x for x in (n, aff, quota) if x)}
+
+
+def ref_driver_render(dae: str, W: int, H: int, spp: int, M: int, threads: int):
+    """Seconds of the reference's own "Rendering... 100%! (Xs)" report (tiles + its per-tile
+    whole-frame tonemap, raytraced_renderer.cpp:595-620,654-682; its timer starts after
+    build_accel), or None."""
     import re
     import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        r = subprocess.run([REF_DRIVER, "-s", str(spp), "-t", str(threads), "-m", str(M), "-r", str(W), str(H),
+                            "-f", os.path.join(td, "ref.png"), os.path.abspath(dae)],
+                           capture_output=True, text=True, timeout=900, cwd=td)
+    m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", r.stdout)
+    return float(m[-1]) if r.returncode == 0 and m else None
+
+
+def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads: int, cores: dict,
+                           min_spp: int = 4):
+    """The reference's own `-t N` CPU path: oracle/_ref/ref_driver (built by __graft_entry__.build()
+    from the reference's sources: RaytracedRenderer + BidirectionalPathTracer, reference flags)
+    rendering the same scene and resolution. The headline figure is a render of `min_spp` spp,
+    where the reference's per-tile whole-frame tonemap (raytraced_renderer.cpp:619, image.h:194-209:
+    2,040 tiles x 2.07 Mpx at 1080p, independent of spp) weighs a quarter of what it does at 1 spp;
+    the 1-spp figure is reported beside it. None when the binary is not present."""
     if not os.path.exists(REF_DRIVER) or not os.path.exists(dae):
         return None
-    done, t_tot, spp_run, runs = 0, 0.0, 1, 0
-    with tempfile.TemporaryDirectory() as td:
-        while t_tot < budget_s * 0.6 and runs < 3:
-            r = subprocess.run([REF_DRIVER, "-s", str(spp_run), "-t", str(threads), "-m", str(M), "-r", str(W),
-                                str(H), "-f", os.path.join(td, "ref.png"), os.path.abspath(dae)],
-                               capture_output=True, text=True, timeout=600, cwd=td)
-            m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", r.stdout)
-            if r.returncode != 0 or not m:
-                return None
-            dt = float(m[-1])
-            t_tot += dt
-            done += W * H * spp_run
-            runs += 1
-            rate = W * H * spp_run / dt
-            spp_run = max(1, int((budget_s - t_tot) * rate / (W * H)))
-    return {"value": done / t_tot / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
-            "sample": f"{name} {W}x{H}, {done // (W * H)} spp, m={M}: the reference's RaytracedRenderer + "
-                      f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2) at -t {threads}, "
-                      f"{t_tot:.1f} s of rendering"}
+    t1 = ref_driver_render(dae, W, H, 1, M, threads)
+    if t1 is None:
+        return None
+    tn = ref_driver_render(dae, W, H, min_spp, M, threads)
+    if tn is None:
+        return None
+    return {"value": W * H * min_spp / tn / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
+            "host": cores,
+            "sample": f"{name} {W}x{H}, {min_spp} spp, m={M}: the reference's RaytracedRenderer + "
+                      f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2) at -t {threads} "
+                      f"(node nproc {cores['nproc']}, usable {cores['usable']}), {tn:.1f} s of rendering",
+            "spp1": {"value": round(W * H / t1 / 1e6, 5), "seconds": round(t1, 2),
+                     "note": "1 spp: the per-tile whole-frame tonemap is a larger share of this time"}}
 
 
-def parity_check(scene, W: int, H: int, M: int, seed: int, rr: bool = False) -> dict:
-    """Per-pixel RMSE of the GPU sample buffer vs the oracle's COUNTER32 CPU path, same seed,
-    same frame at 2 spp (the CPU side of the metric)."""
+def parity_check(scene, W: int, H: int, M: int, seed: int, rr: bool = False, threads: int = 16) -> dict:
+    """The per-pixel quality half of the metric, on the workload's full frame at the same seed,
+    samples 0 and 1 rendered as two 1-spp frames:
+    * rmse: the GPU's 2-spp sample buffer vs oracle COUNTER32 (mode 2: the device's fp32 semantics,
+      tolerance 1e-4);
+    * vs_fp64: the GPU vs oracle COUNTER64 (mode 1: the reference's fp64 arithmetic, same random
+      numbers): per-pixel RMSE, the Monte Carlo noise of the same image, their ratio, and the
+      shares of samples that took another path (fp32 flips) / agree to 1e-5, against the fp32
+      tolerance stated in DESIGN.md §3 (tests/_parity.py)."""
     import numpy as np
     import bdpt_amd as B
-    from _util import MODE_C32, oracle_render
+    from _parity import TOL_AGREE, TOL_DIVERGED, TOL_NOISE_RATIO, fp64_agreement
+    from _util import MODE_C32, MODE_C64, oracle_render
     S = 2
-    pt = B.BidirectionalPathTracer(scene, W, H, S, M, seed=seed, russian_roulette=rr)
-    pt.raytrace_tiles()
-    g = pt.read_frame(B.FRAME_SAMPLE).astype(np.float64)
+    pt = B.BidirectionalPathTracer(scene, W, H, 1, M, seed=seed, russian_roulette=rr)
+    ge, gs = [], []
+    for k in range(S):
+        pt.clear()
+        pt.raytrace_tiles([], k, 1)
+        ge.append(pt.read_frame(B.FRAME_EYE).astype(np.float64))
+        gs.append(pt.read_frame(B.FRAME_SAMPLE).astype(np.float64))
     pt.close()
-    ref = oracle_render(scene, W, H, S, M, MODE_C32, seed=seed,
-                        threads=min(16, os.cpu_count() or 1), rr=rr)[0]
+    o32 = [oracle_render(scene, W, H, 1, M, MODE_C32, seed=seed, s0=k, count=1, threads=threads, rr=rr)
+           for k in range(S)]
+    o64 = [oracle_render(scene, W, H, 1, M, MODE_C64, seed=seed, s0=k, count=1, threads=threads, rr=rr)
+           for k in range(S)]
+    g = np.mean(gs, axis=0)
+    ref = np.mean([o[0] for o in o32], axis=0)
+    agr = fp64_agreement(ge, gs, [o[1] for o in o64], [o[0] for o in o64])
+    agr = {k: (round(v, 8) if isinstance(v, float) else v) for k, v in agr.items()}
+    agr["tolerance"] = {"diverged_frac_max": TOL_DIVERGED, "rmse_over_noise_max": TOL_NOISE_RATIO,
+                        "agree_1e-5_frac_min": TOL_AGREE}
+    agr["cpu"] = "oracle COUNTER64 (the reference's fp64 arithmetic, same counter RNG)"
     return {"rmse": float(np.sqrt(np.mean((g - ref) ** 2))), "spp": S, "frame": f"{W}x{H}",
-            "tolerance": 1e-4, "cpu": "oracle COUNTER32 (fp32 device semantics)"}
+            "tolerance": 1e-4, "cpu": "oracle COUNTER32 (fp32 device semantics)",
+            "rmse_vs_fp64": agr["rmse_vs_fp64"], "diverged_frac_vs_fp64": agr["diverged_frac"],
+            "vs_fp64": agr}
 
 
 def load_traffic(workload: str, kernel_ms: float):
@@ -215,6 +256,13 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong: the workload's fixed render split across ranks (default); "
                          "weak: every rank renders the full spp")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend for N>1: nccl (= RCCL on ROCm, the default) or gloo "
+                         "(same all_reduce of the device frame; lets two ranks share one GPU in tests)")
+    ap.add_argument("--devices", default=None,
+                    help="device of each rank, comma-separated (default: LOCAL_RANK), e.g. 0,0")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the last step's reduced sample frame (.npy, H x W x 3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--scene", default=None, help="override: a .dae path")
@@ -251,14 +299,17 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    devmap = [int(x) for x in args.devices.split(",")] if args.devices else None
+    gpu = devmap[rank % len(devmap)] if devmap else (local if world > 1 else 0)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     t_load = time.perf_counter()
     scene = B.load_dae(scene_path, W, H)      # bdpt_dae_load: the CLI's scene path
@@ -290,20 +341,19 @@ def main() -> int:
     pt.set_stream(stream.cuda_stream)
     t_create = time.perf_counter() - t_create
     frame = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+    # the multi-GPU path (bdpt_amd.ShardedRender): this rank's sample range (or, for the
+    # PathTracer, its row band), the sample frame copied into `frame`, one all-reduce of `frame`
+    sh = B.ShardedRender(pt, frame, rank, world, SPP, scaling, dist)
 
     def render(k: int):
         if use_pt:
             pt.raytrace_tiles(band, 0, SPP)
         else:
-            base, n = rank_sample_range(k, rank, world, SPP, scaling)
-            if n > 0:
-                pt.raytrace_tiles([], base, n)
+            sh.render(k)
 
     for k in range(args.warmup):
         render(k)
-        pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
-        if dist is not None:
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        sh.reduce()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -315,9 +365,7 @@ def main() -> int:
         ev[k][0].record(stream)
         render(args.warmup + k)                     # k_bdpt_sample (k_pt): the dominant kernel
         ev[k][1].record(stream)
-        pt.copy_frame(B.FRAME_SAMPLE, frame.data_ptr())
-        if dist is not None:
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        sh.reduce()                                 # bdpt_copy_frame + all_reduce over the ranks
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -325,18 +373,14 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_samples = int(pt.read_sample_counts().astype(np.int64)[band[0][1]:band[0][1] + band[0][3]].sum()) \
-        if use_pt else W * H * rank_sample_range(0, rank, world, SPP, scaling)[1]
-    rank_elapsed, rank_kern = [elapsed], [kern_ms]
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms, float(rank_samples)], dtype=torch.float64, device=dev)
-        allt = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(allt, t)
-        rank_elapsed = [float(x[0]) for x in allt]
-        rank_kern = [float(x[1]) for x in allt]
-        elapsed = max(rank_elapsed)
-        samples_per_step = sum(float(x[2]) for x in allt)
-    else:
-        samples_per_step = float(rank_samples)
+        if use_pt else W * H * sh.samples(0)
+    rows = sh.gather_floats([elapsed, kern_ms, float(rank_samples), float(gpu)])
+    rank_elapsed = [r[0] for r in rows]
+    rank_kern = [r[1] for r in rows]
+    elapsed = max(rank_elapsed)
+    samples_per_step = sum(r[2] for r in rows)
+    if args.dump_frame and rank == 0:
+        np.save(args.dump_frame, frame.cpu().numpy().reshape(H, W, 3))
     pt.close()
 
     # algorithmic bytes of this rank's launch: in-kernel counters on a separate, untimed launch of
@@ -386,7 +430,8 @@ def main() -> int:
         "config": {"workload": wname
                    + (" unidirectional PathTracer" if use_pt else "")
                    + (", whole frame per step split across GPUs" if scaling == "strong" else ", full spp per GPU")
-                   + (" (row bands)" if use_pt else " (sample ranges)") + " + RCCL sum-reduce",
+                   + (" (row bands)" if use_pt else " (sample ranges)")
+                   + (" + RCCL all-reduce" if args.dist_backend == "nccl" else " + gloo all-reduce"),
                    "workload_key": args.workload if named else "custom",
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
                    "scene": os.path.relpath(scene_path, REPO), "width": W, "height": H, "spp": SPP,
@@ -427,17 +472,21 @@ def main() -> int:
         out["roofline"]["traffic_pmc"] = traffic_info
     if world > 1:
         out["per_rank"] = {"elapsed_s": [round(x, 4) for x in rank_elapsed],
-                           "kernel_ms": [round(x, 3) for x in rank_kern]}
+                           "kernel_ms": [round(x, 3) for x in rank_kern],
+                           "samples_per_step": [int(r[2]) for r in rows], "device": [int(r[3]) for r in rows],
+                           "backend": args.dist_backend}
     if use_pt:
         out["config"]["integrator"] = "PathTracer (pathtracer.cpp:47-340)"
+    cores = host_cores()
+    thr = cores["usable"]
     if world == 1 and not args.no_parity and not use_pt:
-        out["parity"] = parity_check(scene, W, H, M, seed, rr=rr)
+        out["parity"] = parity_check(scene, W, H, M, seed, rr=rr, threads=thr)
     if world == 1 and not args.no_cpu_baseline and not use_pt:
-        thr = min(16, os.cpu_count() or 1)
         port = cpu_baseline(scene, os.path.basename(scene_path), W, H, SPP, M, threads=thr, rr=rr)
         # the reference cannot run the environment light / roulette under BDPT: port only
         ref = (None if (env_desc or rr)
-               else cpu_baseline_reference(scene_path, os.path.basename(scene_path), W, H, M, threads=thr))
+               else cpu_baseline_reference(scene_path, os.path.basename(scene_path), W, H, M, threads=thr,
+                                           cores=cores))
         out["cpu_baseline"] = ref if ref is not None else port
         if ref is not None:   # the oracle port's fp64 path, same host, for comparison
             out["cpu_baseline"]["port"] = {"value": port["value"], "cores": port["cores"], "sample": port["sample"]}

@@ -470,3 +470,66 @@ class PathTracer(BidirectionalPathTracer):
                                   max_tolerance=max_tolerance,
                                   direct_hemisphere_sample=direct_hemisphere_sample,
                                   lens_radius=lens_radius, focal_distance=focal_distance))
+
+
+# --- multi-GPU: one process per GPU under torch.distributed ---------
+# Pixel-samples are independent except the t = 1 light-tracing splats, which land anywhere
+# (bidirection.cpp:457-466), so a frame cannot be split into tiles and gathered: the ranks split
+# the SAMPLE range of every pixel and the W*H*3 frames are summed. The RNG is keyed by the global
+# sample index, so the sum equals one render of all the samples up to fp32 summation order.
+
+
+def rank_sample_range(step: int, rank: int, world: int, spp: int, scaling: str = "strong"):
+    """Global sample indices [begin, begin + count) that `rank` renders in `step`.
+    strong: the step's fixed render of `spp` samples per pixel is split across the ranks;
+    weak: every rank renders a fresh `spp` of its own. Either way every (step, rank) owns a
+    disjoint range, so the summed frames equal one render of all those samples."""
+    if scaling == "strong":
+        lo, hi = spp * rank // world, spp * (rank + 1) // world
+        return step * spp + lo, hi - lo
+    return (step * world + rank) * spp, spp
+
+
+class ShardedRender:
+    """One rank's part of a multi-GPU render: per step, render this rank's sample range of the
+    whole frame (bdpt_render, async on the context's stream), copy the sample frame into `frame`
+    (a float32 tensor of W*H*3 on this rank's device, bdpt_copy_frame) and sum `frame` over the
+    ranks with ONE all-reduce — the only collective (RCCL over xGMI with the "nccl" backend; gloo
+    takes device tensors for all_reduce too, which is how two ranks can share one GPU in tests).
+    A renderer needs raytrace_tiles(tiles, spp_begin, spp_count) and copy_frame(which, ptr) —
+    BidirectionalPathTracer, or any object with the same two calls."""
+
+    def __init__(self, pt, frame, rank: int, world: int, spp: int, scaling: str = "strong", dist=None,
+                 group=None):
+        self.pt, self.frame = pt, frame
+        self.rank, self.world, self.spp, self.scaling = rank, world, spp, scaling
+        self.dist, self.group = dist, group
+
+    def samples(self, step: int) -> int:
+        """sample indices per pixel this rank renders in `step`"""
+        return rank_sample_range(step, self.rank, self.world, self.spp, self.scaling)[1]
+
+    def render(self, step: int) -> None:
+        base, n = rank_sample_range(step, self.rank, self.world, self.spp, self.scaling)
+        if n > 0:
+            self.pt.raytrace_tiles([], base, n)
+
+    def reduce(self) -> None:
+        self.pt.copy_frame(FRAME_SAMPLE, self.frame.data_ptr())
+        if self.dist is not None and self.world > 1:
+            self.dist.all_reduce(self.frame, op=self.dist.ReduceOp.SUM, group=self.group)
+
+    def step(self, step: int) -> None:
+        self.render(step)
+        self.reduce()
+
+    def gather_floats(self, values, device=None):
+        """every rank's `values` (a list of floats), as a list per rank — through all_reduce of a
+        zero-padded (world x n) tensor, which both backends take for device tensors"""
+        import torch
+        v = torch.zeros(self.world, len(values), dtype=torch.float64,
+                        device=device if device is not None else self.frame.device)
+        v[self.rank] = torch.tensor(values, dtype=torch.float64)
+        if self.dist is not None and self.world > 1:
+            self.dist.all_reduce(v, op=self.dist.ReduceOp.SUM, group=self.group)
+        return [[float(x) for x in row] for row in v.cpu()]

@@ -239,6 +239,9 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
     return BDPT_E_INVALID;
   }
   if (d->nmat <= 0 || !d->mats) { err = "scene has no materials"; return BDPT_E_INVALID; }
+  // the path store keeps a vertex's material id in 16 signed bits (bdpt_core.h VtxS::mb; the
+  // negative ids mark environment / camera vertices)
+  if (d->nmat > 32767) { err = "more than 32767 materials (the path vertex stores a 16-bit id)"; return BDPT_E_UNSUPPORTED; }
   if ((d->nlight <= 0 || !d->lights) && !d->envmap) { err = "scene has no light (BDPT needs one)"; return BDPT_E_INVALID; }
   if (d->nprim >= (1 << 24)) { err = "too many primitives for the leaf encoding (2^24)"; return BDPT_E_INVALID; }
   // materials (collada.cpp:854-938 -> bsdf.h classes)

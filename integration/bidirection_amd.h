@@ -9,21 +9,26 @@
 //     +  pt = new BidirectionalPathTracerAMD();
 // Everything else — render_to_file, start_raytracing, the worker threads' raytrace_tile loop of
 // raytrace_pixel calls, write_to_framebuffer after every tile, save_image — runs unmodified:
-//   * start_raytracing calls clear() and set_frame_size(), then sets bvh / camera / scene
-//     (:280-285); the first raytrace_pixel() of the frame attaches the scene (bdpt_create over
-//     scene->objects' primitives in build_accel's collection order, scene->lights, *camera and
-//     envLight's map);
+//   * start_raytracing calls clear() and set_frame_size() on its own thread, then sets bvh /
+//     camera / scene (:280-285); the first raytrace_pixel() of the frame attaches the scene
+//     (bdpt_create over scene->objects' primitives in build_accel's collection order,
+//     scene->lights, *camera and envLight's map);
 //   * the workers call raytrace_pixel() per pixel of a 32x32 tile, row-major (:293-298, 610-615):
-//     the tile's first pixel renders the whole tile with ONE bdpt_render and copies the tile's
-//     pixels of the device frame into sampleBuffer (and sampleCountBuffer = ns_aa, as
-//     bidirection.cpp:539), the others are no-ops, so the write_to_framebuffer after the tile
-//     (:619, non-virtual, pathtracer.cpp:42-45) shows it;
-//   * when the last pixel of the frame has been rendered the whole frame — light-tracing splats
-//     land anywhere (bidirection.cpp:457-466) — goes to sampleBuffer / eyeBuffer / lightBuffer,
-//     so the last write_to_framebuffer and save_image see the final image.
-// A pixel that no 32x32 tile covers (the -p cell path, 8x8 tiles at an arbitrary corner) is a 1x1
-// tile. attach() / raytrace_tile() / raytrace_frame() / finish() remain for callers that drive
-// whole tiles or frames themselves.
+//     the tile's first pixel queues the whole tile (sampleCountBuffer = ns_aa, as
+//     bidirection.cpp:539) and returns; the others are no-ops. Queued tiles go to the device in
+//     batches, one bdpt_render per batch: the worker that finds no launch in flight launches what
+//     is queued, waits for it, copies those pixels into sampleBuffer and repeats while more tiles
+//     were queued meanwhile (by workers that returned at once). A later write_to_framebuffer
+//     (:619, non-virtual, pathtracer.cpp:42-45) shows the tiles whose batch has run;
+//   * the call that queues the frame's last pixel waits for the last batch and then takes the
+//     whole frame — light-tracing splats land anywhere (bidirection.cpp:457-466) — into
+//     sampleBuffer / eyeBuffer / lightBuffer, so the last write_to_framebuffer and save_image see
+//     the final image.
+// A pixel that no 32x32 tile covers (the -p cell path, 8x8 tiles at an arbitrary corner,
+// :300-318) is queued alone; lone pixels of a batch merge into rectangles, and their call returns
+// once its batch is in sampleBuffer (the cell render copies frameBuffer as soon as the workers
+// end, :640-645). attach() / raytrace_tile() / raytrace_frame() / finish() remain for callers that
+// drive whole tiles or frames themselves.
 //
 // Flattening reads the reference's scene objects: Triangle p1..p3 / n1..n3, Sphere o / r, the
 // BSDF parameters, the light fields and the camera (hFov, vFov, nClip, fClip, pos, c2w, w2c). The
@@ -32,13 +37,18 @@
 // compile check in tests/test_integration.py builds it with the same read access the oracle's
 // ref_driver uses.
 //
-// Threading: the reference's worker threads call raytrace_pixel concurrently (on disjoint tiles);
-// the binding's tile bookkeeping is under a mutex, and bdpt_render serialises launches per context.
+// Threading: the reference's worker threads call raytrace_pixel concurrently (on disjoint tiles).
+// The per-pixel "queued" flags are allocated while the renderer is single-threaded
+// (set_frame_size); the queue, the counters and every bdpt_* call on the context are under one
+// mutex, released while a batch runs on the device (only the launching thread touches the
+// context then).
 #ifndef BDPT_AMD_INTEGRATION_BIDIRECTION_AMD_H
 #define BDPT_AMD_INTEGRATION_BIDIRECTION_AMD_H
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -139,8 +149,15 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   }
 
   // ---- the PathTracer contract, driven by the reference's unmodified RaytracedRenderer ----
+  // start_raytracing calls clear() and then set_frame_size() before it starts the workers
+  // (raytraced_renderer.cpp:280-281, 326): the per-pixel flags are allocated, zeroed, here.
   void set_frame_size(size_t width, size_t height) override {
     BidirectionalPathTracer::set_frame_size(width, height);
+    drop_frame();
+  }
+  // start_raytracing (:280) clears before every frame: the next raytrace_pixel attaches again
+  void clear() override {
+    BidirectionalPathTracer::clear();
     drop_frame();
   }
   // The renderer's per-pixel call (raytraced_renderer.cpp:610-615; bidirection.cpp:503-542). It
@@ -148,23 +165,42 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // (no device, bdpt_* error) is recorded — error() — and the frame's remaining pixels are skipped.
   void raytrace_pixel(size_t x, size_t y) override {
     const size_t W = sampleBuffer.w, H = sampleBuffer.h;
-    if (x >= W || y >= H || failed_.load(std::memory_order_acquire)) return;
-    if (done_ && done_[x + y * W].load(std::memory_order_acquire)) return;   // rendered with its tile
-    std::lock_guard<std::mutex> lk(mu_);
+    if (x >= W || y >= H || !done_ || failed_.load(std::memory_order_acquire)) return;
+    if (done_[x + y * W].load(std::memory_order_acquire)) return;   // queued with its tile
+    std::unique_lock<std::mutex> lk(mu_);
     if (failed_.load(std::memory_order_relaxed)) return;
     try {
-      render_pixel_locked(x, y, W, H);
+      const bool lone = enqueue_locked(x, y, W, H);
+      const size_t mine = seq_;
+      pump(lk);
+      if (lone)   // -p cell path: return once this pixel is in sampleBuffer
+        cv_.wait(lk, [&] { return copied_ >= mine || failed_.load(); });
+      if (queued_ == W * H && !finished_ && !failed_.load()) {
+        // the frame's last pixel: wait for the batch in flight, then take the whole frame
+        cv_.wait(lk, [&] { return !launching_ || failed_.load(); });
+        if (!failed_.load() && !finished_) {
+          finished_ = true;
+          finish();   // every splat is in (bidirection.cpp:457-466): sampleBuffer <- the image
+        }
+      }
     } catch (const std::exception& e) {
-      err_ = e.what();
-      failed_.store(true, std::memory_order_release);
+      record_failure_locked(e.what());
     }
   }
   // empty, or the first failure of the frame's raytrace_pixel calls
-  std::string error() const { return failed_.load() ? err_ : std::string(); }
-  size_t launches() const { return launches_; }   // bdpt_render calls since the last frame reset
+  std::string error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return failed_.load() ? err_ : std::string();
+  }
+  size_t launches() { std::lock_guard<std::mutex> lk(mu_); return launches_; }   // bdpt_render calls this frame
+  size_t tiles_queued() { std::lock_guard<std::mutex> lk(mu_); return seq_; }    // tiles / lone pixels queued
+  // seconds the launching threads spent in bdpt_render + the batches' copies into sampleBuffer
+  double device_seconds() { std::lock_guard<std::mutex> lk(mu_); return busy_s_; }
 
  private:
-  void render_pixel_locked(size_t x, size_t y, size_t W, size_t H) {
+  // Queues the tile whose first pixel (x, y) is — tiles start at multiples of imageTileSize = 32,
+  // raytraced_renderer.cpp:83,293-298 — or else the pixel alone (returns true then). mu_ held.
+  bool enqueue_locked(size_t x, size_t y, size_t W, size_t H) {
     if (!ctx_) {
       if (!scene || !camera) throw std::runtime_error("BidirectionalPathTracerAMD: no scene / camera");
       std::vector<SceneObjects::Primitive*> prims;   // build_accel's collection order (:352-360)
@@ -175,33 +211,109 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       const HDRImageBuffer* env = envLight ? static_cast<const SceneObjects::EnvironmentLight*>(envLight)->envMap : nullptr;
       check(attach(prims, scene->lights, *camera, env));
     }
-    if (!done_) {
-      done_.reset(new std::atomic<uint8_t>[W * H]);
-      for (size_t k = 0; k < W * H; k++) done_[k].store(0, std::memory_order_relaxed);
-      rendered_ = 0;
-    }
-    if (done_[x + y * W].load(std::memory_order_relaxed)) return;
-    // the tile whose first pixel this is (tiles start at multiples of imageTileSize = 32,
-    // raytraced_renderer.cpp:83,293-298), else this pixel alone
+    if (done_[x + y * W].load(std::memory_order_relaxed)) return false;
     const bool corner = x % kTile == 0 && y % kTile == 0;
     const size_t tw = corner ? std::min(kTile, W - x) : 1, th = corner ? std::min(kTile, H - y) : 1;
-    raytrace_tile((int)x, (int)y, (int)tw, (int)th);
     for (size_t yy = y; yy < y + th; yy++)
       for (size_t xx = x; xx < x + tw; xx++) {
         sampleCountBuffer[xx + yy * W] = ns_aa;   // bidirection.cpp:539
-        if (!done_[xx + yy * W].exchange(1, std::memory_order_release)) rendered_++;
+        if (!done_[xx + yy * W].exchange(1, std::memory_order_release)) queued_++;
       }
-    if (rendered_ == W * H) {
-      finish();   // the frame is complete: every splat is in, sampleBuffer <- the whole image
-    } else {
-      std::vector<float> rgb(tw * th * 3);
-      check(bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, (int32_t)x, (int32_t)y, (int32_t)tw, (int32_t)th, rgb.data()));
-      for (size_t yy = 0; yy < th; yy++)
-        for (size_t xx = 0; xx < tw; xx++) {
-          const float* v = &rgb[3 * (xx + yy * tw)];
-          sampleBuffer.data[(x + xx) + (y + yy) * W] = Vector3D(v[0], v[1], v[2]);
+    pending_.push_back(bdpt_tile{(int32_t)x, (int32_t)y, (int32_t)tw, (int32_t)th});
+    seq_++;
+    return !corner;
+  }
+
+  // Launches the queued tiles in batches. The caller that finds no launch in flight becomes the
+  // launcher and goes on until nothing is queued; tiles queued meanwhile by the other workers
+  // (who return at once) go out together in the next bdpt_render. mu_ held on entry and exit,
+  // released while the device works.
+  void pump(std::unique_lock<std::mutex>& lk) {
+    if (launching_) return;
+    launching_ = true;
+    while (!pending_.empty() && !failed_.load()) {
+      std::vector<bdpt_tile> batch;
+      batch.swap(pending_);
+      const size_t upto = seq_;
+      coalesce(batch);
+      lk.unlock();
+      const auto t0 = std::chrono::steady_clock::now();
+      int rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
+      if (rc == BDPT_OK) rc = copy_back(batch);   // waits for the launch
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      lk.lock();
+      launches_++;
+      busy_s_ += dt;
+      copied_ = upto;
+      if (rc != BDPT_OK) record_failure_locked(bdpt_last_error());
+      cv_.notify_all();
+    }
+    launching_ = false;
+    cv_.notify_all();
+  }
+
+  // sampleBuffer <- the batch's pixels: one rectangle read per tile for a few tiles, else one
+  // whole-frame read.
+  int copy_back(const std::vector<bdpt_tile>& batch) {
+    const size_t W = sampleBuffer.w;
+    std::vector<float> rgb;
+    if (batch.size() > 16) {
+      rgb.resize(W * sampleBuffer.h * 3);
+      int rc = bdpt_read_frame(ctx_, BDPT_FRAME_SAMPLE, rgb.data());
+      if (rc != BDPT_OK) return rc;
+      for (const bdpt_tile& t : batch)
+        for (int32_t yy = t.y0; yy < t.y0 + t.h; yy++)
+          for (int32_t xx = t.x0; xx < t.x0 + t.w; xx++) {
+            const float* v = &rgb[3 * (xx + yy * W)];
+            sampleBuffer.data[xx + yy * W] = Vector3D(v[0], v[1], v[2]);
+          }
+      return BDPT_OK;
+    }
+    for (const bdpt_tile& t : batch) {
+      rgb.resize((size_t)t.w * t.h * 3);
+      int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, t.x0, t.y0, t.w, t.h, rgb.data());
+      if (rc != BDPT_OK) return rc;
+      for (int32_t yy = 0; yy < t.h; yy++)
+        for (int32_t xx = 0; xx < t.w; xx++) {
+          const float* v = &rgb[3 * (xx + yy * t.w)];
+          sampleBuffer.data[(t.x0 + xx) + (t.y0 + yy) * W] = Vector3D(v[0], v[1], v[2]);
         }
     }
+    return BDPT_OK;
+  }
+
+  // Lone pixels merge into rectangles: runs along a row, then equal runs on consecutive rows (an
+  // 8x8 cell tile becomes one tile instead of 64 one-pixel blocks). The set of pixels, and so the
+  // image, is unchanged.
+  static void coalesce(std::vector<bdpt_tile>& batch) {
+    std::vector<bdpt_tile> out, px;
+    for (const bdpt_tile& t : batch) (t.w == 1 && t.h == 1 ? px : out).push_back(t);
+    if (px.size() < 2) return;
+    std::sort(px.begin(), px.end(), [](const bdpt_tile& a, const bdpt_tile& b) {
+      return a.y0 != b.y0 ? a.y0 < b.y0 : a.x0 < b.x0;
+    });
+    std::vector<bdpt_tile> runs;
+    for (const bdpt_tile& p : px) {
+      if (!runs.empty() && runs.back().y0 == p.y0 && runs.back().x0 + runs.back().w == p.x0) runs.back().w++;
+      else runs.push_back(p);
+    }
+    std::sort(runs.begin(), runs.end(), [](const bdpt_tile& a, const bdpt_tile& b) {
+      return a.x0 != b.x0 ? a.x0 < b.x0 : a.w != b.w ? a.w < b.w : a.y0 < b.y0;
+    });
+    std::vector<bdpt_tile> rects;
+    for (const bdpt_tile& r : runs) {
+      bdpt_tile* b = rects.empty() ? nullptr : &rects.back();
+      if (b && b->x0 == r.x0 && b->w == r.w && b->y0 + b->h == r.y0) b->h++;
+      else rects.push_back(r);
+    }
+    out.insert(out.end(), rects.begin(), rects.end());
+    batch.swap(out);
+  }
+
+  void record_failure_locked(const std::string& what) {
+    if (!failed_.load()) err_ = what;
+    failed_.store(true, std::memory_order_release);
+    cv_.notify_all();
   }
 
  public:
@@ -213,11 +325,6 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   void raytrace_frame() {
     check(bdpt_render(ctx_, nullptr, 0, 0, (int32_t)ns_aa));
     launches_++;
-  }
-  // start_raytracing (:280) clears before every frame: the next raytrace_pixel attaches again
-  void clear() override {
-    BidirectionalPathTracer::clear();
-    drop_frame();
   }
   // sampleBuffer / eyeBuffer / lightBuffer <- the device frames, before save_image
   void finish() {
@@ -260,12 +367,17 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     }
     return m;
   }
-  void drop_frame() {   // a new frame (size / scene / camera may have changed): attach again
+  // a new frame (size / scene / camera may have changed): attach again. Called on the renderer's
+  // thread with no worker running (set_frame_size / clear, :280-281).
+  void drop_frame() {
     std::lock_guard<std::mutex> lk(mu_);
     if (ctx_) { bdpt_destroy(ctx_); ctx_ = nullptr; }
-    done_.reset();
-    rendered_ = 0;
-    launches_ = 0;
+    const size_t n = sampleBuffer.w * sampleBuffer.h;
+    done_.reset(n ? new std::atomic<uint8_t>[n]() : nullptr);   // value-initialised: all 0
+    pending_.clear();
+    queued_ = seq_ = copied_ = launches_ = 0;
+    busy_s_ = 0.0;
+    launching_ = finished_ = false;
     failed_.store(false);
     err_.clear();
   }
@@ -287,8 +399,14 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   static constexpr size_t kTile = 32;   // RaytracedRenderer::imageTileSize (raytraced_renderer.cpp:83)
   void* ctx_ = nullptr;
   std::mutex mu_;
-  std::unique_ptr<std::atomic<uint8_t>[]> done_;   // per pixel: rendered with its tile
-  size_t rendered_ = 0, launches_ = 0;
+  std::condition_variable cv_;
+  std::unique_ptr<std::atomic<uint8_t>[]> done_;   // per pixel: queued (with its tile)
+  std::vector<bdpt_tile> pending_;                 // queued, not yet launched
+  size_t queued_ = 0;                              // pixels queued this frame
+  size_t seq_ = 0, copied_ = 0;                    // tiles queued / tiles whose batch is in sampleBuffer
+  size_t launches_ = 0;
+  double busy_s_ = 0.0;
+  bool launching_ = false, finished_ = false;
   std::atomic<bool> failed_{false};
   std::string err_;
   std::vector<int32_t> type_, mat_;

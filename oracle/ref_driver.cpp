@@ -30,6 +30,7 @@
 #include <thread>
 #include <mutex>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <stack>
 #include <random>
@@ -246,10 +247,10 @@ int main(int argc, char** argv) {
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
   std::string png = "/dev/null", npy_prefix, scene_json, cam_settings;
-  bool render = true, uni = false, amd = false, amd_loop = false;
+  bool render = true, uni = false, amd = false, amd_loop = false, tile_loop = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GA")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GAB")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -269,6 +270,7 @@ int main(int argc, char** argv) {
       case 'c': cam_settings = optarg; break;            // main.cpp:120-121
       case 'G': amd = true; break;                       // integration check (BDPT_INTEGRATION builds)
       case 'A': amd_loop = true; break;                  // the binding under the reference's own render loop
+      case 'B': amd_loop = true; tile_loop = true; break;   // ... its worker loop without the per-tile tonemap
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -412,6 +414,59 @@ int main(int argc, char** argv) {
     return 2;
 #endif
   }
+#ifdef BDPT_INTEGRATION
+  if (tile_loop) {
+    // -B: the binding's own throughput. The reference's worker loop (raytraced_renderer.cpp:
+    // 654-666 -> raytrace_tile :595-617: `threads` workers take the 32x32 tiles of
+    // start_raytracing's queue in raster order, :293-298, and call raytrace_pixel on every pixel,
+    // row-major) WITHOUT the whole-frame write_to_framebuffer after each tile (:619), whose cost
+    // grows with the frame's pixels times its tiles and does not depend on the integrator. The
+    // scene is attached (bdpt_create: BVH build + upload, the reference's build_accel) before
+    // the timer starts.
+    amd_pt->clear();
+    amd_pt->set_frame_size(screenW, screenH);
+    std::vector<SceneObjects::Primitive*> prims;
+    for (SceneObjects::SceneObject* obj : rr->scene->objects) {
+      const std::vector<SceneObjects::Primitive*>& op = obj->get_primitives();
+      prims.insert(prims.end(), op.begin(), op.end());
+    }
+    amd_pt->bvh = rr->bvh; amd_pt->camera = &camera; amd_pt->scene = rr->scene;
+    const int rc = amd_pt->attach(prims, rr->scene->lights, camera, envmap);
+    if (rc != BDPT_OK) {
+      fprintf(stderr, "[ref_driver] BidirectionalPathTracerAMD::attach: %d (%s)\n", rc, bdpt_last_error());
+      return 20 - rc;
+    }
+    const size_t T = 32;
+    std::vector<std::pair<size_t, size_t>> tiles;
+    for (size_t y = 0; y < screenH; y += T)
+      for (size_t x = 0; x < screenW; x += T) tiles.emplace_back(x, y);
+    std::atomic<size_t> next{0};
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ws;
+    for (size_t t = 0; t < threads; t++)
+      ws.emplace_back([&] {
+        for (size_t k; (k = next.fetch_add(1)) < tiles.size();)
+          for (size_t y = tiles[k].second; y < std::min(tiles[k].second + T, screenH); y++)
+            for (size_t x = tiles[k].first; x < std::min(tiles[k].first + T, screenW); x++) amd_pt->raytrace_pixel(x, y);
+      });
+    for (auto& w : ws) w.join();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!amd_pt->error().empty()) {
+      fprintf(stderr, "[ref_driver] BidirectionalPathTracerAMD: %s\n", amd_pt->error().c_str());
+      return 24;
+    }
+    fprintf(stdout, "[ref_driver] binding tile loop: %.4f s, %.3f Msamples/s, %zu tiles, %zu bdpt_render "
+            "launches, %.4f s in launches\n", secs, (double)screenW * screenH * ns_aa / secs * 1e-6,
+            amd_pt->tiles_queued(), amd_pt->launches(), amd_pt->device_seconds());
+    if (!npy_prefix.empty()) {
+      write_npy(npy_prefix + "_sample.npy", amd_pt->sampleBuffer);
+      write_npy(npy_prefix + "_eye.npy", amd_pt->eyeBuffer);
+      write_npy(npy_prefix + "_light.npy", amd_pt->lightBuffer);
+    }
+    return 0;
+  }
+  std::chrono::steady_clock::time_point loop_t0 = std::chrono::steady_clock::now();
+#endif
   try {
     rr->render_to_file(png, (size_t)-1, 0, 0, 0);
   } catch (const std::exception& e) {   // the binding reports bdpt_* failures as exceptions
@@ -423,7 +478,10 @@ int main(int argc, char** argv) {
     fprintf(stderr, "[ref_driver] BidirectionalPathTracerAMD: %s\n", amd_pt->error().c_str());
     return amd_pt->error() == "no HIP device" ? 23 : 24;
   }
-  if (amd_pt) fprintf(stdout, "[ref_driver] bdpt_render launches: %zu\n", amd_pt->launches());
+  if (amd_pt)
+    fprintf(stdout, "[ref_driver] bdpt_render launches: %zu for %zu tiles; %.4f s in launches of %.4f s in "
+            "render_to_file\n", amd_pt->launches(), amd_pt->tiles_queued(), amd_pt->device_seconds(),
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - loop_t0).count());
 #endif
   if (!npy_prefix.empty() && uni) {
     write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);

@@ -184,3 +184,15 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
     }
   return 0;
 }
+
+// the device tree's depth and node count (binary tree before the 4-wide collapse), as built under
+// the current BDPT_BVH / BDPT_SAH_* settings
+extern "C" int core_cpu_dev_tree(const bdpt_scene_desc* d, int* depth, int* nodes) {
+  HostScene hs;
+  std::string err;
+  int rc = build_host_scene(d, hs, err);
+  if (rc) return rc;
+  *depth = hs.dev_depth;
+  *nodes = hs.dev_nodes;
+  return 0;
+}

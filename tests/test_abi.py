@@ -71,6 +71,29 @@ def test_ambient_light_rejected_under_bdpt_only():
     assert lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx)) == B.BDPT_E_UNSUPPORTED
 
 
+def test_material_id_range_rejected_before_device():
+    """The path store keeps a vertex's material id in 16 signed bits (bdpt_core.h VtxS): a scene
+    with 32,768 materials is rejected with BDPT_E_UNSUPPORTED instead of wrapping on the device;
+    32,767 passes the scene checks (and then needs a device)."""
+    sc = golden_scene("CBspheres", 32, 24)
+    lib = B.load_library()
+    p = B.Params()
+    p.width, p.height, p.spp, p.max_depth = 32, 24, 1, 5
+    ctx = C.c_void_p()
+    for n, unsupported in ((32768, True), (32767, False)):
+        mats = [sc.mats[i] for i in range(sc.nmat)] + [sc.mats[0]] * (n - sc.nmat)
+        big = B.Scene(sc.prim_type, sc.prim_geom, sc.prim_mat.copy(), mats,
+                      [sc.lights[i] for i in range(sc.nlight)], sc.camera)
+        big.prim_mat[0] = n - 1   # the last material is used
+        rc = lib.bdpt_create(C.byref(big.desc()), C.byref(p), C.byref(ctx))
+        assert (rc == B.BDPT_E_UNSUPPORTED) == unsupported, (n, rc, lib.bdpt_last_error())
+        if unsupported:
+            assert b"32767" in lib.bdpt_last_error()
+        if ctx.value:
+            lib.bdpt_destroy(ctx)
+            ctx = C.c_void_p()
+
+
 def test_bad_frame_size_rejected():
     sc = golden_scene("CBspheres", 32, 24)
     p = B.Params()

@@ -147,3 +147,46 @@ def test_triangle_early_outs_exact(tmp_path):
     out = subprocess.run([exe, "1000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "mismatches 0" in out.stdout
+
+
+@pytest.mark.parametrize("env", [{"BDPT_BVH": "ref"}, {"BDPT_SAH_LEAF": "1"}, {"BDPT_SAH_LEAF": "2", "BDPT_SAH_CT": "0.25"},
+                                 {"BDPT_SAH_BINS": "4", "BDPT_SAH_CT": "4"}], ids=["ref", "leaf1", "leaf2_ct", "bins4"])
+@pytest.mark.parametrize("scene,W,H,spp,M", [("scenes/CBgems.dae", 32, 24, 1, 7), ("scenes/CBbunny.dae", 40, 30, 1, 5)])
+def test_device_tree_knobs_bit_exact(scene, W, H, spp, M, env, monkeypatch):
+    """The device tree's shape changes no result (closest hits by t, equal-t ties by the reference
+    tree's leaf order): BDPT_BVH=ref builds the device tree from the reference's own
+    midpoint tree (bvh.cpp:51-129) instead of the binned SAH; BDPT_SAH_LEAF / _CT / _BINS change
+    the SAH tree's leaf size, termination cost and bin count. Each is bit-exact vs mode 2."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = B.load_dae(os.path.join(REPO, scene), W, H)
+    for lm in (0, 1):
+        eye, light, _ = core_render(sc, W, H, spp, M, seed=5, lds_mode=lm)
+        _, oeye, olight, _ = oracle_render(sc, W, H, spp, M, MODE_C32, seed=5, threads=1)
+        assert np.array_equal(eye, oeye) and np.array_equal(light, olight), (env, lm)
+
+
+def test_device_tree_knobs_change_the_tree(monkeypatch):
+    """...and they do select another tree: BDPT_BVH=ref has the reference tree's depth and node
+    count (19 / 18,565 for CBbunny, tests/golden/scenes/facts.json), the default SAH tree others,
+    and a SAH leaf size of 1 more nodes than the default's."""
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "scenes", "facts.json")) as f:
+        facts = json.load(f)["CBbunny"]
+    sc = B.load_dae(os.path.join(REPO, "scenes", "CBbunny.dae"), 32, 24)
+    lib = core()
+    lib.core_cpu_dev_tree.restype = C.c_int
+
+    def tree(**env):
+        for k in ("BDPT_BVH", "BDPT_SAH_LEAF"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        depth, nodes = C.c_int(), C.c_int()
+        assert lib.core_cpu_dev_tree(C.byref(sc.desc()), C.byref(depth), C.byref(nodes)) == 0
+        return depth.value, nodes.value
+
+    assert tree(BDPT_BVH="ref") == (facts["bvh_depth"], facts["bvh_nodes"])
+    sah = tree()
+    assert sah != (facts["bvh_depth"], facts["bvh_nodes"])
+    assert tree(BDPT_SAH_LEAF="1")[1] > sah[1]

@@ -352,6 +352,21 @@ def test_standin_c5_shaped(lds, monkeypatch):
     _check_frames(g, oracle_render(sc, W, H, S, M, MODE_C32, rr=True), f"stand-in + env + RR m8 LM {lds}")
 
 
+@pytest.mark.parametrize("env", [{"BDPT_BVH": "ref"}, {"BDPT_SAH_LEAF": "1"},
+                                 {"BDPT_SAH_BINS": "4", "BDPT_SAH_CT": "4"}], ids=["ref_tree", "leaf1", "bins4"])
+@pytest.mark.parametrize("scene", ["standin", "CBgems"])
+def test_device_tree_knobs(scene, env, monkeypatch):
+    """The device traversing the reference's own midpoint tree (BDPT_BVH=ref, bvh.cpp:51-129) or
+    other SAH trees (BDPT_SAH_LEAF / _CT / _BINS) renders the same image: the tree's shape decides
+    no result. The stand-in runs the treelet + HBM kernel (LM 2), CBgems the
+    whole-scene-in-LDS one (LM 1)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    W, H, S, M = (256, 144, 2, 5) if scene == "standin" else (160, 120, 2, 7)
+    sc = _standin(W, H) if scene == "standin" else golden_scene("CBgems", W, H)
+    _check_frames(_gpu_render(sc, W, H, S, M), oracle_render(sc, W, H, S, M, MODE_C32), f"{scene} {env}")
+
+
 @pytest.mark.parametrize("env", [{"BDPT_XCD_GROUPS": "1"}, {"BDPT_BLOCK_MAJOR": "0"},
                                  {"BDPT_XCD_GROUPS": "1", "BDPT_BLOCK_MAJOR": "0"}])
 def test_ticket_orders(env, monkeypatch):

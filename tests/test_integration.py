@@ -82,7 +82,8 @@ def test_render_loop_binding_fails_cleanly_without_device(tmp_path):
 @pytest.mark.parametrize("scene,W,H,S,M", [("CBspheres", 200, 150, 2, 5), ("CBgems", 160, 100, 2, 7)])
 def test_reference_render_loop_through_binding(tmp_path, scene, W, H, S, M):
     """The reference's unmodified render_to_file at -t 8 with BidirectionalPathTracerAMD in place:
-    one bdpt_render per 32x32 tile (raytraced_renderer.cpp:293-298), the PNG its own save_image
+    every 32x32 tile (raytraced_renderer.cpp:293-298) queued once, in at most one bdpt_render per
+    tile (the binding batches the tiles queued while a launch runs), the PNG its own save_image
     writes equal to the product CLI's at the same seed (light-image splats are fp32 atomics in
     another order, so a byte may differ by one step where a value sits on a quantisation
     boundary), its sampleBuffer / eyeBuffer / lightBuffer within the parity tolerance of the
@@ -94,7 +95,8 @@ def test_reference_render_loop_through_binding(tmp_path, scene, W, H, S, M):
     assert "Rendering... 100%!" in r.stdout and "Job completed" in r.stdout
     ntiles = ((W + 31) // 32) * ((H + 31) // 32)
     launches = int(r.stdout.split("bdpt_render launches:")[1].split()[0])
-    assert launches == ntiles, (launches, ntiles)
+    queued = int(r.stdout.split("bdpt_render launches:")[1].split()[2])
+    assert queued == ntiles and 1 <= launches <= ntiles, (launches, queued, ntiles)
     sc = B.load_dae(os.path.join(REPO, "scenes", scene + ".dae"), W, H)
     samp, eye, light, _ = oracle_render(sc, W, H, S, M, MODE_C32)
     for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
@@ -111,3 +113,45 @@ def test_reference_render_loop_through_binding(tmp_path, scene, W, H, S, M):
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.001 * d.size
     rate_ref = read_png(tmp_path / "loop_rate.png")
     assert np.array_equal(rate_ref, read_png(tmp_path / "cli_rate.png"))
+
+
+def _run_tile_loop(tmp_path, scene, W, H, S, M, threads=8):
+    """-B: the reference's worker loop (raytrace_tile's raytrace_pixel calls over the 32x32 tile
+    queue, `threads` workers) through the binding, without the per-tile whole-frame tonemap."""
+    prefix = str(tmp_path / "tl")
+    r = subprocess.run([AMD, "-B", "-t", str(threads), "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-o", prefix,
+                        os.path.join(REPO, "scenes", scene + ".dae")], capture_output=True, text=True, timeout=300,
+                       cwd=tmp_path)
+    return r, prefix
+
+
+@needs_bin
+def test_tile_loop_fails_cleanly_without_device(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present: the GPU test covers the binding")
+    r, _ = _run_tile_loop(tmp_path, "CBspheres", 64, 48, 2, 5)
+    assert r.returncode == 23, r.stdout + r.stderr
+    assert "no HIP device" in r.stderr
+
+
+@needs_bin
+@pytest.mark.gpu
+def test_tile_loop_batches_and_matches_oracle(tmp_path):
+    """All tiles queued exactly once, fewer launches than tiles (batched), and the frame equal to
+    oracle mode 2 within the GPU parity tolerance."""
+    import bdpt_amd as B
+    W, H, S, M = 320, 240, 2, 5
+    r, prefix = _run_tile_loop(tmp_path, "CBspheres", W, H, S, M)
+    assert r.returncode == 0, r.stdout + r.stderr
+    print(r.stdout)
+    line = r.stdout.split("binding tile loop:")[1]
+    tiles = int(line.split(" tiles")[0].split(",")[-1])
+    launches = int(line.split(" bdpt_render")[0].split(",")[-1])
+    ntiles = ((W + 31) // 32) * ((H + 31) // 32)
+    assert tiles == ntiles and 1 <= launches < ntiles, (tiles, launches, ntiles)
+    sc = B.load_dae(os.path.join(REPO, "scenes", "CBspheres.dae"), W, H)
+    samp, eye, light, _ = oracle_render(sc, W, H, S, M, MODE_C32)
+    for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
+        ours = np.load(f"{prefix}_{name}.npy")
+        assert float(np.sqrt(np.mean((ours - ref) ** 2))) < 1e-4, name

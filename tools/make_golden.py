@@ -40,6 +40,11 @@ RENDERS = [
     ("CBspheres", 96, 72, 3, 1, False),
     ("CBspheres", 96, 72, 1, 8, False),
     ("CBbunny", 80, 60, 1, 5, False),
+    # higher-spp renders for the per-pixel statistical bridge between the reference's own
+    # mt19937 stream and the counter-RNG modes (tests/test_bridge.py)
+    ("CBspheres", 64, 48, 64, 5, True),
+    ("CBgems", 64, 48, 64, 7, True),
+    ("CBbunny", 64, 48, 64, 5, True),
 ]
 
 
@@ -63,30 +68,37 @@ def run(scene, W, H, S, M, out_prefix, json_path=None, render=True):
 
 
 def main():
+    only = sys.argv[1:]   # optional render keys: regenerate just those (index entries merged)
     if not os.path.exists(DRIVER):
         sys.exit("build oracle/_ref first: make -f oracle/ref.mk -j8")
     os.makedirs(os.path.join(GOLD, "scenes"), exist_ok=True)
     os.makedirs(os.path.join(GOLD, "hdr"), exist_ok=True)
     tmp = tempfile.mkdtemp()
-    for s in SCENES:
+    for s in ([] if only else SCENES):
         run(s, 480, 360, 1, 1, os.path.join(tmp, s), os.path.join(GOLD, "scenes", s + ".json"),
             render=False)
     # BVH facts of the large mesh (scene JSON too big to commit): dump to tmp, keep the stats.
-    bunny_json = os.path.join(tmp, "CBbunny.json")
-    run("CBbunny", 480, 360, 1, 1, os.path.join(tmp, "CBbunny"), bunny_json, render=False)
-    with open(bunny_json) as f:
-        bj = json.load(f)
-    facts = {"CBbunny": {"nprim": len(bj["prim_order"]), "bvh_nodes": bj["bvh"]["nodes"],
-                         "bvh_leaves": bj["bvh"]["leaves"], "bvh_depth": bj["bvh"]["depth"],
-                         "camera": bj["camera"], "lights": bj["lights"],
-                         "materials": bj["materials"],
-                         "scene_sha256": hashlib.sha256(json.dumps(
-                             [bj["triangles"], bj["spheres"]]).encode()).hexdigest()}}
-    with open(os.path.join(GOLD, "scenes", "facts.json"), "w") as f:
-        json.dump(facts, f, indent=1)
+    if not only:
+        bunny_json = os.path.join(tmp, "CBbunny.json")
+        run("CBbunny", 480, 360, 1, 1, os.path.join(tmp, "CBbunny"), bunny_json, render=False)
+        with open(bunny_json) as f:
+            bj = json.load(f)
+        facts = {"CBbunny": {"nprim": len(bj["prim_order"]), "bvh_nodes": bj["bvh"]["nodes"],
+                             "bvh_leaves": bj["bvh"]["leaves"], "bvh_depth": bj["bvh"]["depth"],
+                             "camera": bj["camera"], "lights": bj["lights"],
+                             "materials": bj["materials"],
+                             "scene_sha256": hashlib.sha256(json.dumps(
+                                 [bj["triangles"], bj["spheres"]]).encode()).hexdigest()}}
+        with open(os.path.join(GOLD, "scenes", "facts.json"), "w") as f:
+            json.dump(facts, f, indent=1)
     index = {}
+    if only:
+        with open(os.path.join(GOLD, "hdr", "index.json")) as f:
+            index = json.load(f)
     for scene, W, H, S, M, keep in RENDERS:
         key = f"{scene}_{W}x{H}_s{S}_m{M}"
+        if only and key not in only:
+            continue
         pre = os.path.join(tmp, key)
         rays, isects = run(scene, W, H, S, M, pre)
         bufs = {n: np.load(f"{pre}_{n}.npy") for n in ("sample", "eye", "light")}
