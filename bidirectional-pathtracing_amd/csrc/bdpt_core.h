@@ -1529,15 +1529,25 @@ struct PathsInRegs {
   BDPT_HD Vtx l(int k) const { return vtx_load<EXT>(P.L[k - 1]); }
 };
 
-// Eye and light subpaths of one pixel-sample plus their MIS constants
-// (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524;
-// prepare_bidirectional_subpath :20-102 for both walks). The two walks run as ONE loop: a lane whose
-// eye walk ends starts its light walk in the next iteration, so a wave iterates
-// max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
-// sample + walk: 1) make the interleaving invisible in the results.
-template <int MAXV, int LM = 0, bool EXT = false>
-BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
-                            int x, int y, uint32_t sample) {
+// The next vertex's throughput alpha = prev_alpha * |cos| * f / pdf (prepare_bidirectional_subpath
+// :60-62), formed when its ray is: one f3 live across the traversal instead of alpha, f and pdf
+BDPT_HD f3 walk_next_alpha(f3 pa, f3 pn, f3 d, f3 f, float pdf) { return divs(mul(muls(pa, fabsf(dot(pn, d))), f), pdf); }
+
+// The state of one lane's fused eye + light walk between two iterations (walk_step).
+struct WalkState {
+  f3 ro, rd, prev_n, nalpha;   // the next ray, the previous vertex's normal, the next vertex's throughput
+  float rmin, rmax;
+  float pv_fwd, pv_gp, pv_q;   // the previous vertex's fwd / prefix / roulette probability
+  int i, count, pv_mat;        // reference vertex index, vertices stored on this subpath, previous material
+  uint32_t dm, lpos;           // delta mask of this subpath; the light stream's position after L[1]
+  bool light, l1env;           // walking the light subpath; its L[1] is an environment vertex
+};
+
+// Starts one pixel-sample's walk: the camera ray (raytrace_pixel's jitter, bidirection.cpp:515-524)
+// and the light vertex L[1] with the light walk's first ray (sample_light_ray, :105-118).
+template <int MAXV, bool EXT = false>
+BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
+                        WalkState& w, int x, int y, uint32_t sample) {
   rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
   float px, py;
   grid2d(g, &px, &py);
@@ -1634,25 +1644,38 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
   cnt.clk_light += __builtin_amdgcn_s_memtime() - tl0;
 #endif
-  const uint32_t lpos = gl0.pos;
+  w.lpos = gl0.pos;
   P.l1_d = ld;
   P.l1_pdf = ldp;
-  l1env = false;   // re-read with the rest when the light walk starts
+  w.l1env = false;   // re-read with the rest when the light walk starts
   // the walk: eye first (camera ray on [nClip, fClip], alpha = 1, pdf = 1, n = d), then light
-  f3 ro = cam;
-  float rmin = S.cam.nclip, rmax = S.cam.fclip;
-  f3 prev_n = rd;
-  // the next vertex's throughput alpha = prev_alpha * |cos| * f / pdf (prepare_bidirectional_subpath
-  // :60-62), formed when its ray is: one f3 live across the traversal instead of alpha, f and pdf
-  auto next_alpha = [](f3 pa, f3 pn, f3 d, f3 f, float pdf) { return divs(mul(muls(pa, fabsf(dot(pn, d))), f), pdf); };
-  f3 nalpha = next_alpha(divs(splat3(1.0f), 1.0f), prev_n, rd, splat3(1.0f), 1.0f);
-  int i = 2, count = 0;
-  uint32_t dm = 0;
-  bool light = false;
-  // the previous vertex's material / fwd / prefix / roulette probability (fused constants)
-  int pv_mat = -1;
-  float pv_fwd = 1.0f, pv_gp = 0.0f, pv_q = 1.0f;
-  for (;;) {
+  w.ro = cam;
+  w.rmin = S.cam.nclip;
+  w.rmax = S.cam.fclip;
+  w.prev_n = rd;
+  w.rd = rd;
+  w.nalpha = walk_next_alpha(divs(splat3(1.0f), 1.0f), rd, rd, splat3(1.0f), 1.0f);
+  w.i = 2;
+  w.count = 0;
+  w.dm = 0;
+  w.light = false;
+  w.pv_mat = -1;
+  w.pv_fwd = 1.0f; w.pv_gp = 0.0f; w.pv_q = 1.0f;
+}
+// One iteration of the fused walk: trace the next ray, store the vertex it hits (with its MIS
+// constants), sample the continuation. Returns true once the light subpath has ended (both
+// subpaths and P.nE / P.nL / P.dE / P.dL complete).
+template <int MAXV, int LM = 0, bool EXT = false>
+BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
+                       WalkState& w) {
+  f3 ro = w.ro, rd = w.rd, prev_n = w.prev_n, nalpha = w.nalpha;
+  float rmin = w.rmin, rmax = w.rmax, pv_fwd = w.pv_fwd, pv_gp = w.pv_gp, pv_q = w.pv_q;
+  int i = w.i, count = w.count, pv_mat = w.pv_mat;
+  uint32_t dm = w.dm;
+  bool light = w.light, l1env = w.l1env;
+  auto next_alpha = walk_next_alpha;
+  bool done = false;
+  {
     Hit h;
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
@@ -1789,23 +1812,43 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
       if (light) {
         P.nL = count + 2;
         P.dL = dm;
-        break;
-      }
+        done = true;
+      } else {
       P.nE = count + 2;
       P.dE = dm;
       light = true;
       // the light sample drawn before the eye walk, read back from the path store (not held in
       // registers across the eye walk)
       rng_stream(g, 1);
-      g.pos = lpos;
+      g.pos = w.lpos;
       ro = P.L[0].pos; rd = P.l1_d; prev_n = P.L[0].n;
       nalpha = next_alpha(P.L[0].alpha, prev_n, rd, splat3(1.0f), P.l1_pdf);
-      mis_p = P.L[0].fwd;
+      const float mis_p = P.L[0].fwd;
       l1env = vs_mat(P.L[0]) == (int)MAT_ENV_V;
       rmin = BDPT_EPS_F; rmax = INFINITY;
       i = 2; count = 0; dm = 0;
       pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
+      }
     }
+  }
+  w.ro = ro; w.rd = rd; w.prev_n = prev_n; w.nalpha = nalpha;
+  w.rmin = rmin; w.rmax = rmax; w.pv_fwd = pv_fwd; w.pv_gp = pv_gp; w.pv_q = pv_q;
+  w.i = i; w.count = count; w.pv_mat = pv_mat; w.dm = dm; w.light = light; w.l1env = l1env;
+  return done;
+}
+
+// Eye and light subpaths of one pixel-sample plus their MIS constants
+// (est_radiance_global_illumination, bidirection.cpp:472-488; raytrace_pixel :515-524;
+// prepare_bidirectional_subpath :20-102 for both walks). The two walks run as ONE loop: a lane whose
+// eye walk ends starts its light walk in the next iteration, so a wave iterates
+// max(|E| + |L|) times instead of max |E| + max |L|. The RNG sub-streams (eye walk: 0, light
+// sample + walk: 1) make the interleaving invisible in the results.
+template <int MAXV, int LM = 0, bool EXT = false>
+BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
+                            int x, int y, uint32_t sample) {
+  WalkState w;
+  walk_begin<MAXV, EXT>(S, sp, P, cnt, g, w, x, y, sample);
+  while (!walk_step<MAXV, LM, EXT>(S, sp, P, cnt, g, w)) {
   }
 }
 

@@ -235,11 +235,14 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       std::vector<bdpt_tile> batch;
       batch.swap(pending_);
       const size_t upto = seq_;
+      // the frame's last batch: finish() reads the whole frame right after it, so its own copy
+      // into sampleBuffer is skipped (only its completion is waited for)
+      const bool last = queued_ == sampleBuffer.w * sampleBuffer.h;
       coalesce(batch);
       lk.unlock();
       const auto t0 = std::chrono::steady_clock::now();
       int rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
-      if (rc == BDPT_OK) rc = copy_back(batch);   // waits for the launch
+      if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch);   // waits for the launch
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       lk.lock();
       launches_++;
@@ -326,16 +329,23 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     check(bdpt_render(ctx_, nullptr, 0, 0, (int32_t)ns_aa));
     launches_++;
   }
-  // sampleBuffer / eyeBuffer / lightBuffer <- the device frames, before save_image
+  // sampleBuffer / eyeBuffer / lightBuffer <- the device frames, before save_image. The sample
+  // frame is the fp32 sum eye + light (what bdpt_read_frame(BDPT_FRAME_SAMPLE) returns, formed here
+  // from the two frames already read).
   void finish() {
     const size_t n = sampleBuffer.w * sampleBuffer.h;
-    std::vector<float> rgb(n * 3);
-    HDRImageBuffer* dst[3] = {&sampleBuffer, &eyeBuffer, &lightBuffer};
-    const int32_t which[3] = {BDPT_FRAME_SAMPLE, BDPT_FRAME_EYE, BDPT_FRAME_LIGHT};
-    for (int b = 0; b < 3; b++) {
-      if (dst[b]->w * dst[b]->h != n) continue;
-      check(bdpt_read_frame(ctx_, which[b], rgb.data()));
-      for (size_t k = 0; k < n; k++) dst[b]->data[k] = Vector3D(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+    std::vector<float> eye(n * 3), light(n * 3);
+    check(bdpt_read_frame(ctx_, BDPT_FRAME_EYE, eye.data()));
+    check(bdpt_read_frame(ctx_, BDPT_FRAME_LIGHT, light.data()));
+    const bool el = eyeBuffer.w * eyeBuffer.h == n && lightBuffer.w * lightBuffer.h == n;
+    for (size_t k = 0; k < n; k++) {
+      const float* e = &eye[3 * k];
+      const float* l = &light[3 * k];
+      sampleBuffer.data[k] = Vector3D(e[0] + l[0], e[1] + l[1], e[2] + l[2]);
+      if (el) {
+        eyeBuffer.data[k] = Vector3D(e[0], e[1], e[2]);
+        lightBuffer.data[k] = Vector3D(l[0], l[1], l[2]);
+      }
     }
   }
   ~BidirectionalPathTracerAMD() {

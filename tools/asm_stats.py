@@ -15,7 +15,7 @@ import sys
 from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CS = os.path.join(ROOT, "bidirectional-pathtracing_amd", "csrc")
+CS = os.environ.get('ASM_CS', os.path.join(ROOT, 'bidirectional-pathtracing_amd', 'csrc'))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
