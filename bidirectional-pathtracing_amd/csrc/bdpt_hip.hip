@@ -141,8 +141,11 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
 // mbcnt compaction) into the wave's LDS ring, and whenever 64 are queued the whole wave traces
 // them together — all 64 lanes busy on shadow rays regardless of per-lane path lengths.
-constexpr int kMinWaves = 4;   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
-constexpr int kBlock = 1024;   // one block per CU: one LDS scene copy shared by its 16 waves
+#ifndef BDPT_WAVES
+#define BDPT_WAVES 4
+#endif
+constexpr int kMinWaves = BDPT_WAVES;   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
+constexpr int kBlock = 256 * kMinWaves; // one block per CU: one LDS scene copy shared by its 16 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
 // Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
@@ -585,7 +588,7 @@ __global__ void k_combine(const float* a, const float* b, float* out, long long 
 constexpr size_t kLdsPerCu = 160 * 1024;
 // scenes up to this many primitives use the flat leaf-list traversal (LM 3)
 constexpr int kFlatMaxPrims = 24;   // flat leaf list up to this many primitives; measured: CBspheres 488 -> 511 Msamples/s, CBspheres_lambertian +6%, CBempty -1%
-constexpr size_t kBlocksPerCu = 16 / kWavesPerBlock;
+constexpr size_t kBlocksPerCu = 4 * kMinWaves / kWavesPerBlock;
 constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256 - kStaticLds;
 
 // Persistent launch: as many blocks as are co-resident (occupancy query with this launch's LDS),

@@ -109,9 +109,14 @@ Frame<R> make_coord_space(const V3<R>& n) {
 // which take Z = n for a hit normal (already unit length: the intersection normalises it) instead
 // of normalising it again (bdpt_core.h make_frame_hit); modes 0 and 1 (fp64) keep
 // the reference's make_coord_space, so mode 0 stays bit-exact with the reference.
+// oracle_set_hit_frame_ref(1): mode 2 with the reference's make_coord_space for hits too (the
+// device semantics minus the Z = n shortcut), so tests can bound what the shortcut alone changes.
+static int g_hit_frame_ref = 0;
+extern "C" void oracle_set_hit_frame_ref(int on) { g_hit_frame_ref = on; }
+
 template <class R>
 Frame<R> hit_coord_space(const V3<R>& n) {
-  if (!std::is_same<R, float>::value) return make_coord_space(n);
+  if (!std::is_same<R, float>::value || g_hit_frame_ref) return make_coord_space(n);
   V3<R> z(n.x, n.y, n.z);
   V3<R> h = z;
   if (std::fabs(h.x) <= std::fabs(h.y) && std::fabs(h.x) <= std::fabs(h.z))

@@ -53,6 +53,8 @@ def oracle():
         lib.oracle_cos_sin_2pi.restype = None
         lib.oracle_mt_first.argtypes = [C.c_int, P]
         lib.oracle_mt_first.restype = C.c_double
+        lib.oracle_set_hit_frame_ref.argtypes = [C.c_int]
+        lib.oracle_set_hit_frame_ref.restype = None
         _oracle = lib
     return _oracle
 
