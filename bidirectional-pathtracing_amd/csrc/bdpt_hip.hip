@@ -141,11 +141,11 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
 // in the reference's order; every connection that needs a visibility ray is pushed (ballot +
 // mbcnt compaction) into the wave's LDS ring, and whenever 64 are queued the whole wave traces
 // them together — all 64 lanes busy on shadow rays regardless of per-lane path lengths.
-#ifndef BDPT_WAVES
-#define BDPT_WAVES 4
-#endif
-constexpr int kMinWaves = BDPT_WAVES;   // 128 VGPRs: measured best (2: 160, 3: 220, 4: 259, 5: 151 Msamples/s)
-constexpr int kBlock = 256 * kMinWaves; // one block per CU: one LDS scene copy shared by its 16 waves
+// 4 waves per SIMD = 128 VGPRs: measured best (round 1: 2: 160, 3: 220, 4: 259, 5: 151 Msamples/s;
+// round 4, with 0 instead of 38-51 spilled VGPRs at 3 waves: still -13..-16% on every workload,
+// profiles/r04c_ab_waves.log)
+constexpr int kMinWaves = 4;
+constexpr int kBlock = 256 * kMinWaves;   // one block per CU: one LDS scene copy shared by its 16 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
 // Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
