@@ -31,7 +31,11 @@ if [ "${PART:-check}" = check ]; then
   step bench_c2 900 python bench.py --workload c2
 fi
 if [ "${PART}" = tests ]; then
-  step pytest_gpu 1500 $PYT tests -m gpu
+  step pytest_gpu 1100 $PYT tests -m gpu
+fi
+if [ "${PART}" = full ]; then   # the round's record: GPU tests, then every BASELINE workload's bench line
+  step pytest_gpu 600 $PYT tests -m gpu
+  PART=bench
 fi
 if [ "${PART}" = bench ]; then
   for w in ${WORKLOADS:-ns c2 c3 c4 c5}; do
