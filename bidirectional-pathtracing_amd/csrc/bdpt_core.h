@@ -269,6 +269,8 @@ struct SceneView {
   int fn;                // LM 3: > 0 when the leaves hold primitives 0 .. fn-1 in order (flat_prims)
   uint32_t fsph;         // LM 3: sphere mask of those primitives
   int ntop;
+  int* lstack;           // LM 2: the traversal stacks' first kLdsStack overflow slots in LDS (slot k of
+                         // lane t at lstack[k * kLdsStackStride + t]); null: all overflow in scratch
   DCam cam;
   EnvView env;
 };
@@ -414,19 +416,54 @@ BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 // Traversal stack: the newest K entries in registers (shifted on push/pop, fully unrolled), older
 // ones in a private array (K = 0: all of it). Near-first traversal of these trees rarely holds more
 // than ~8 entries; a few register entries keep most pushes/pops off scratch.
+// The overflow below the register entries: its first kLdsStack slots in LDS when the kernel gives
+// the stack an LDS area (SceneView::lstack, LM 2; one lane's slot k at lstack[k * stride + lane], no
+// bank conflicts), deeper ones in the private array. A pop from LDS puts the next node address on
+// the critical path after an LDS read instead of a scratch (L1 / L2) read. The 32 KB come out of the
+// LM-2 treelet (~430 -> ~180 nodes). Measured (profiles/r04i_ab_lds_stack.log, Msamples/s, 0 / 4 /
+// 8 / 12 slots): north star 681 / 690 / 689 / 679, C5-shaped 580 / 586 / 590 / 579, C3 465 / 471 /
+// 471 / 465, CBbunny 800x600 510 / 517 / 515 / 508.
+constexpr int kLdsStack = 8;
+constexpr int kLdsStackStride = 1024;   // lanes per block (bdpt_hip.hip kBlock)
+
+// this lane's LDS overflow slots (device, LM 2 kernels that staged them), else null
+BDPT_HD int* lane_stack(const SceneView& S) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return kLdsStack > 0 && S.lstack ? S.lstack + threadIdx.x : nullptr;
+#else
+  return nullptr;
+#endif
+}
+
 template <int K>
 struct TravStack {
   int s[K > 0 ? K : 1];
   int nreg, msp;
   int* mem;   // a separate private array, so that s[] / nreg / msp stay in registers
-  BDPT_HD explicit TravStack(int* m) : nreg(0), msp(0), mem(m) {}
+  int* lds;   // this lane's LDS overflow slots (stride kLdsStackStride), or null
+  BDPT_HD explicit TravStack(int* m, int* l = nullptr) : nreg(0), msp(0), mem(m), lds(l) {}
   BDPT_HD void clear() { nreg = 0; msp = 0; }
-  BDPT_HD void push(int v) {
-    if (K == 0) {
-      mem[msp++] = v;
+  BDPT_HD void put(int k, int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (kLdsStack > 0 && lds && k < kLdsStack) {
+      *(__attribute__((address_space(3))) int*)(lds + k * kLdsStackStride) = v;
       return;
     }
-    if (nreg == K) mem[msp++] = s[K - 1];
+#endif
+    mem[k] = v;
+  }
+  BDPT_HD int get(int k) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (kLdsStack > 0 && lds && k < kLdsStack) return *(const __attribute__((address_space(3))) int*)(lds + k * kLdsStackStride);
+#endif
+    return mem[k];
+  }
+  BDPT_HD void push(int v) {
+    if (K == 0) {
+      put(msp++, v);
+      return;
+    }
+    if (nreg == K) put(msp++, s[K - 1]);
     else nreg++;
 #pragma unroll
     for (int k = K - 1; k > 0; k--) s[k] = s[k - 1];
@@ -441,7 +478,7 @@ struct TravStack {
       return true;
     }
     if (msp == 0) return false;
-    v = mem[--msp];
+    v = get(--msp);
     return true;
   }
 };
@@ -660,7 +697,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   h.key = -1;
   h.b1 = 0; h.b2 = 0;
   int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem);
+  TravStack<K> stk(stack_mem, LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.closest++;
   int li = 0;
@@ -779,7 +816,7 @@ template <int LM = 0, int K = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
   RayInv r = make_rayinv(o, d);
   int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem);
+  TravStack<K> stk(stack_mem, LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.shadow++;
   int li = 0;

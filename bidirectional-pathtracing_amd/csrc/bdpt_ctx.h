@@ -100,6 +100,7 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.nleaves = (int)c->hs.leaf_refs.size();
   S.fn = flat_prims(c->hs, &S.fsph);
   S.ntop = 0;
+  S.lstack = nullptr;
   S.cam = c->hs.cam;
   const HostScene& hs = c->hs;
   S.env.light = hs.env_light;

@@ -159,6 +159,7 @@ constexpr bool conn_compact() { return kConnCompact == 1 || (kConnCompact == 2 &
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
 // (measured: C2 +3%, Lucy stand-in +1%, CBgems +1%)
 constexpr int kLdsMats = 48, kLdsLights = 8;
+constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 2 only
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
 
 #ifdef BDPT_PHASE_PROF
@@ -172,8 +173,12 @@ constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLig
 // materials / lights, and points kp.S at them.
 template <int LM>
 __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DMat* s_mats, DLight* s_lights) {
+  if (LM == 2 && kLdsStack > 0) {   // the traversal stacks' LDS overflow slots, behind the wave queues
+    static_assert(kLdsStackStride == kBlock, "LDS stack stride = lanes per block");
+    kp.S.lstack = (int*)(smem + kWavesPerBlock * sizeof(WaveQ));
+  }
   if (LM != 0) {
-    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ));
+    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ) + (LM == 2 ? kLdsStackBytes : 0));
     const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
@@ -620,10 +625,11 @@ int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
   if (lm == 2 && !has_nodes) lm = 0;
   kp.S = view_of(c, lm);
   kp.n_node4 = (int)(c->hs.tree(lm_width(lm)).nodes.size() / 4);
-  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top, kLdsSceneMax / node_bytes(lm_width(2)));
+  if (lm == 2) kp.S.ntop = (int)std::min<size_t>((size_t)c->hs.tree(lm_width(2)).n_top,
+                                                 (kLdsSceneMax - kLdsStackBytes) / node_bytes(lm_width(2)));
   if (lm == 2 && c->env_ntop_max >= 0) kp.S.ntop = std::min(kp.S.ntop, c->env_ntop_max);   // diagnostics
   c->last_lm = lm;
-  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
+  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? kLdsStackBytes + (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
   return lm;
 }
 
