@@ -64,3 +64,35 @@ def test_counter_fp32_mode_matches_reference_per_pixel(key, scene, M):
     print(key, "reference", np.round(r["ref_tails"], 4), round(r["ref_mean_z"], 3), "nulls",
           np.round(r["null_tails"].mean(0), 4), np.round(r["null_mean_z"], 3))
     check_tails(r, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,scene,M", HI_SPP)
+def test_gpu_matches_reference_per_pixel(key, scene, M):
+    """The same per-pixel bridge with the GPU in place of mode 2: libbdpt_amd.so's 64-spp frame
+    against the reference binary's own (tools/make_golden.py), the null from independent GPU
+    frames."""
+    import bdpt_amd as B
+    g, ref = hi_spp_fixture(key)
+    W, H, S = g["W"], g["H"], g["spp"]
+    sc = B.load_dae(os.path.join(REPO, "scenes", scene + ".dae"), W, H)
+
+    def frames(s0, n, count):   # `count` frames of n samples each, from global sample s0 on
+        pt = B.BidirectionalPathTracer(sc, W, H, n, M, seed=5489)
+        out = []
+        try:
+            for k in range(count):
+                pt.clear()
+                pt.raytrace_tiles([], s0 + k * n, n)
+                out.append(pt.read_frame(B.FRAME_SAMPLE).astype(np.float64))
+        finally:
+            pt.close()
+        return out
+
+    A = frames(0, S, 1)[0]
+    var1 = np.array(frames(S, 1, N_VAR)).var(0, ddof=1)
+    nulls = frames(S + N_VAR, S, N_NULL)
+    r = null_calibrated_tails(ref, A, nulls, var1, S)
+    print(key, "reference", np.round(r["ref_tails"], 4), round(r["ref_mean_z"], 3), "nulls",
+          np.round(r["null_tails"].mean(0), 4), np.round(r["null_mean_z"], 3))
+    check_tails(r, key)
