@@ -269,7 +269,7 @@ struct SceneView {
   int fn;                // LM 3: > 0 when the leaves hold primitives 0 .. fn-1 in order (flat_prims)
   uint32_t fsph;         // LM 3: sphere mask of those primitives
   int ntop;
-  int* lstack;           // LM 2: the traversal stacks' first kLdsStack overflow slots in LDS (slot k of
+  int* lstack;           // LM 1 / 2: the traversal stacks' first kLdsStack overflow slots in LDS (slot k of
                          // lane t at lstack[k * kLdsStackStride + t]); null: all overflow in scratch
   DCam cam;
   EnvView env;
@@ -419,7 +419,7 @@ BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 // ones in a private array (K = 0: all of it). Near-first traversal of these trees rarely holds more
 // than ~8 entries; a few register entries keep most pushes/pops off scratch.
 // The overflow below the register entries: its first kLdsStack slots in LDS when the kernel gives
-// the stack an LDS area (SceneView::lstack, LM 2; one lane's slot k at lstack[k * stride + lane], no
+// the stack an LDS area (SceneView::lstack, LM 1 / 2; one lane's slot k at lstack[k * stride + lane], no
 // bank conflicts), deeper ones in the private array. A pop from LDS puts the next node address on
 // the critical path after an LDS read instead of a scratch (L1 / L2) read. The 32 KB come out of the
 // LM-2 treelet (~430 -> ~180 nodes). Measured (profiles/r04i_ab_lds_stack.log, Msamples/s, 0 / 4 /
@@ -428,7 +428,7 @@ BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 constexpr int kLdsStack = 8;
 constexpr int kLdsStackStride = 1024;   // lanes per block (bdpt_hip.hip kBlock)
 
-// this lane's LDS overflow slots (device, LM 2 kernels that staged them), else null
+// this lane's LDS overflow slots (device, LM 1 / 2 kernels that staged them), else null
 BDPT_HD int* lane_stack(const SceneView& S) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return kLdsStack > 0 && S.lstack ? S.lstack + threadIdx.x : nullptr;
@@ -699,7 +699,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   h.key = -1;
   h.b1 = 0; h.b2 = 0;
   int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem, LM == 2 ? lane_stack(S) : nullptr);
+  TravStack<K> stk(stack_mem, LM == 1 || LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.closest++;
   int li = 0;
@@ -818,7 +818,7 @@ template <int LM = 0, int K = 0>
 BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c) {
   RayInv r = make_rayinv(o, d);
   int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem, LM == 2 ? lane_stack(S) : nullptr);
+  TravStack<K> stk(stack_mem, LM == 1 || LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.shadow++;
   int li = 0;

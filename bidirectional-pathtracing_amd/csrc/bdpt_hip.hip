@@ -50,6 +50,7 @@ struct KParams {
   int n_node4, n_geom4;       // float4 counts of the node / geometry arrays (LDS staging)
   int nmat;
   unsigned item_lo;           // first item of this launch (tickets count from it)
+  int lstack_on;              // the traversal stacks' LDS overflow slots are staged (LM 1 / 2)
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -159,7 +160,8 @@ constexpr bool conn_compact() { return kConnCompact == 1 || (kConnCompact == 2 &
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
 // (measured: C2 +3%, Lucy stand-in +1%, CBgems +1%)
 constexpr int kLdsMats = 48, kLdsLights = 8;
-constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 2 only
+constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 1 (when it fits) and 2
+
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
 
 #ifdef BDPT_PHASE_PROF
@@ -173,12 +175,12 @@ constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLig
 // materials / lights, and points kp.S at them.
 template <int LM>
 __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DMat* s_mats, DLight* s_lights) {
-  if (LM == 2 && kLdsStack > 0) {   // the traversal stacks' LDS overflow slots, behind the wave queues
-    static_assert(kLdsStackStride == kBlock, "LDS stack stride = lanes per block");
+  static_assert(kLdsStackStride == kBlock, "LDS stack stride = lanes per block");
+  const bool lst = (LM == 1 || LM == 2) && kLdsStack > 0 && kp.lstack_on;
+  if (lst)   // the traversal stacks' LDS overflow slots, behind the wave queues
     kp.S.lstack = (int*)(smem + kWavesPerBlock * sizeof(WaveQ));
-  }
   if (LM != 0) {
-    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ) + (LM == 2 ? kLdsStackBytes : 0));
+    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ) + (lst ? kLdsStackBytes : 0));
     const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
@@ -629,7 +631,11 @@ int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
                                                  (kLdsSceneMax - kLdsStackBytes) / node_bytes(lm_width(2)));
   if (lm == 2 && c->env_ntop_max >= 0) kp.S.ntop = std::min(kp.S.ntop, c->env_ntop_max);   // diagnostics
   c->last_lm = lm;
-  *lds = q + (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? kLdsStackBytes + (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
+  // LM 2 always gives the stacks their LDS slots (the treelet makes room); LM 1 when the whole
+  // scene and the slots fit together (CBgems: +0.5 .. +0.8 %, profiles/r04o_ab_stack_lm1.log)
+  kp.lstack_on = lm == 2 || (lm == 1 && full + kLdsStackBytes <= kLdsSceneMax);
+  *lds = q + (kp.lstack_on ? kLdsStackBytes : 0) +
+         (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
   return lm;
 }
 
@@ -852,6 +858,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.n_geom4 = (int)(c->hs.geom.size() / 4);
   kp.nmat = (int)c->hs.mats.size();
   kp.item_lo = 0;
+  kp.lstack_on = 0;
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);
