@@ -17,9 +17,10 @@
 //     the tile's first pixel queues the whole tile (sampleCountBuffer = ns_aa, as
 //     bidirection.cpp:539) and returns; the others are no-ops. Queued tiles go to the device in
 //     batches, one bdpt_render per batch: the worker that finds no launch in flight launches what
-//     is queued, waits for it, copies those pixels into sampleBuffer and repeats while more tiles
-//     were queued meanwhile (by workers that returned at once). A later write_to_framebuffer
-//     (:619, non-virtual, pathtracer.cpp:42-45) shows the tiles whose batch has run;
+//     is queued, waits for it, copies those pixels into sampleBuffer (batches of up to 16 tiles;
+//     a larger one waits for the frame's end) and repeats while more tiles were queued meanwhile
+//     (by workers that returned at once). A later write_to_framebuffer (:619, non-virtual,
+//     pathtracer.cpp:42-45) shows the tiles whose batch has been copied;
 //   * the call that queues the frame's last pixel waits for the last batch and then takes the
 //     whole frame — light-tracing splats land anywhere (bidirection.cpp:457-466) — into
 //     sampleBuffer / eyeBuffer / lightBuffer, so the last write_to_framebuffer and save_image see
@@ -54,6 +55,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bdpt/bdpt.h"
@@ -255,23 +257,14 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     cv_.notify_all();
   }
 
-  // sampleBuffer <- the batch's pixels: one rectangle read per tile for a few tiles, else one
-  // whole-frame read.
+  // sampleBuffer <- the batch's pixels, one rectangle read per tile. A large batch (more than 16
+  // tiles: the workers queued faster than the device rendered, as without the reference's per-tile
+  // tonemap) is not copied: finish() brings the whole frame in when the last pixel is queued, and
+  // the copy would only delay the next launch.
   int copy_back(const std::vector<bdpt_tile>& batch) {
+    if (batch.size() > 16) return bdpt_sync(ctx_);
     const size_t W = sampleBuffer.w;
     std::vector<float> rgb;
-    if (batch.size() > 16) {
-      rgb.resize(W * sampleBuffer.h * 3);
-      int rc = bdpt_read_frame(ctx_, BDPT_FRAME_SAMPLE, rgb.data());
-      if (rc != BDPT_OK) return rc;
-      for (const bdpt_tile& t : batch)
-        for (int32_t yy = t.y0; yy < t.y0 + t.h; yy++)
-          for (int32_t xx = t.x0; xx < t.x0 + t.w; xx++) {
-            const float* v = &rgb[3 * (xx + yy * W)];
-            sampleBuffer.data[xx + yy * W] = Vector3D(v[0], v[1], v[2]);
-          }
-      return BDPT_OK;
-    }
     for (const bdpt_tile& t : batch) {
       rgb.resize((size_t)t.w * t.h * 3);
       int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, t.x0, t.y0, t.w, t.h, rgb.data());
@@ -329,24 +322,41 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     check(bdpt_render(ctx_, nullptr, 0, 0, (int32_t)ns_aa));
     launches_++;
   }
+  // After attach(): one untimed one-pixel launch (the process's first launch loads the kernel's
+  // code object), then the frames are cleared again — for hosts that time their frames.
+  void warm_up() {
+    bdpt_tile t = {0, 0, 1, 1};
+    check(bdpt_render(ctx_, &t, 1, 0, 1));
+    check(bdpt_sync(ctx_));
+    check(bdpt_clear(ctx_));
+    check(bdpt_sync(ctx_));
+  }
   // sampleBuffer / eyeBuffer / lightBuffer <- the device frames, before save_image. The sample
   // frame is the fp32 sum eye + light (what bdpt_read_frame(BDPT_FRAME_SAMPLE) returns, formed here
-  // from the two frames already read).
+  // from the two frames already read). The conversion to the reference's double buffers (3 x W*H
+  // Vector3D) is split over up to 16 host threads: 1080p is 6 M vectors.
   void finish() {
     const size_t n = sampleBuffer.w * sampleBuffer.h;
     std::vector<float> eye(n * 3), light(n * 3);
     check(bdpt_read_frame(ctx_, BDPT_FRAME_EYE, eye.data()));
     check(bdpt_read_frame(ctx_, BDPT_FRAME_LIGHT, light.data()));
     const bool el = eyeBuffer.w * eyeBuffer.h == n && lightBuffer.w * lightBuffer.h == n;
-    for (size_t k = 0; k < n; k++) {
-      const float* e = &eye[3 * k];
-      const float* l = &light[3 * k];
-      sampleBuffer.data[k] = Vector3D(e[0] + l[0], e[1] + l[1], e[2] + l[2]);
-      if (el) {
-        eyeBuffer.data[k] = Vector3D(e[0], e[1], e[2]);
-        lightBuffer.data[k] = Vector3D(l[0], l[1], l[2]);
+    auto convert = [&](size_t k0, size_t k1) {
+      for (size_t k = k0; k < k1; k++) {
+        const float* e = &eye[3 * k];
+        const float* l = &light[3 * k];
+        sampleBuffer.data[k] = Vector3D(e[0] + l[0], e[1] + l[1], e[2] + l[2]);
+        if (el) {
+          eyeBuffer.data[k] = Vector3D(e[0], e[1], e[2]);
+          lightBuffer.data[k] = Vector3D(l[0], l[1], l[2]);
+        }
       }
-    }
+    };
+    const size_t nt = std::max<size_t>(1, std::min<size_t>({16, (size_t)std::thread::hardware_concurrency(), n / 65536 + 1}));
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(convert, n * t / nt, n * (t + 1) / nt);
+    convert(0, n / nt);
+    for (std::thread& x : th) x.join();
   }
   ~BidirectionalPathTracerAMD() {
     if (ctx_) bdpt_destroy(ctx_);
