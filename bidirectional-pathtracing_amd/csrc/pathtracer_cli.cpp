@@ -18,6 +18,7 @@
 // the timer starts, as the reference's starts after build_accel. The report's ray / test counts
 // come from a second, untimed render of the same samples by the instrumented kernel (--no-stats
 // skips it).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -261,7 +262,19 @@ int main(int argc, char** argv) {
   const std::vector<double> hdr(img.begin(), img.end());
   const std::vector<uint32_t> rgba = bdpt::tonemap(hdr.data(), w, h);
   fprintf(stderr, "[PathTracer] Saving to file: %s... ", out.c_str());
-  if (!bdpt::write_png(out, rgba, w, h)) { fprintf(stderr, "failed\n"); return 1; }
+  if (tiles.empty()) {
+    if (!bdpt::write_png(out, rgba, w, h)) { fprintf(stderr, "failed\n"); return 1; }
+  } else {
+    // the cell render saves the cell only (raytrace_cell copies the cell of the frame buffer into a
+    // dx x dy buffer, save_image writes that, raytraced_renderer.cpp:622-646, 690-728); the rate
+    // image below stays whole-frame, as save_sampling_rate_image reads the whole sampleCountBuffer
+    const int x0 = std::max(0L, cx), y0 = std::max(0L, cy);
+    const int cw = std::max(0, (int)std::min((long)w, cx + cdx) - x0), ch = std::max(0, (int)std::min((long)h, cy + cdy) - y0);
+    std::vector<uint32_t> cell((size_t)cw * ch);
+    for (int y = 0; y < ch; y++)
+      for (int x = 0; x < cw; x++) cell[(size_t)y * cw + x] = rgba[(size_t)(y0 + y) * w + x0 + x];
+    if (!bdpt::write_png(out, cell, cw, ch)) { fprintf(stderr, "failed\n"); return 1; }
+  }
   fprintf(stderr, "Done!\n");
   std::vector<float> rate((size_t)w * h, 0.0f);
   if (pt) {   // sampleCountBuffer[k] * 1.0f / ns_aa (save_sampling_rate_image, raytraced_renderer.cpp:737)

@@ -240,11 +240,11 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       // the frame's last batch: finish() reads the whole frame right after it, so its own copy
       // into sampleBuffer is skipped (only its completion is waited for)
       const bool last = queued_ == sampleBuffer.w * sampleBuffer.h;
-      coalesce(batch);
+      const bool lone = coalesce(batch);
       lk.unlock();
       const auto t0 = std::chrono::steady_clock::now();
       int rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
-      if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch);   // waits for the launch
+      if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch, lone);   // waits for the launch
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       lk.lock();
       launches_++;
@@ -257,14 +257,27 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     cv_.notify_all();
   }
 
-  // sampleBuffer <- the batch's pixels, one rectangle read per tile. A large batch (more than 16
-  // tiles: the workers queued faster than the device rendered, as without the reference's per-tile
-  // tonemap) is not copied: finish() brings the whole frame in when the last pixel is queued, and
-  // the copy would only delay the next launch.
-  int copy_back(const std::vector<bdpt_tile>& batch) {
-    if (batch.size() > 16) return bdpt_sync(ctx_);
+  // sampleBuffer <- the batch's pixels, one rectangle read per tile. A large batch of whole tiles
+  // (more than 16: the workers queued faster than the device rendered, as without the reference's
+  // per-tile tonemap) is not copied: finish() brings the whole frame in when the last pixel is
+  // queued, and the copy would only delay the next launch. A batch with lone pixels (their
+  // callers wait for them, -p cell path) refreshes every queued pixel.
+  int copy_back(const std::vector<bdpt_tile>& batch, bool lone) {
+    if (batch.size() > 16 && !lone) return bdpt_sync(ctx_);
     const size_t W = sampleBuffer.w;
     std::vector<float> rgb;
+    if (lone) {
+      // The -p cell path never queues the whole frame, so finish() never runs: every batch
+      // refreshes all pixels queued so far, so the splats of later samples (bidirection.cpp:
+      // 457-466) reach the cell's earlier pixels too, and the cell's last batch leaves it complete.
+      rgb.resize(W * sampleBuffer.h * 3);
+      int rc = bdpt_read_frame(ctx_, BDPT_FRAME_SAMPLE, rgb.data());
+      if (rc != BDPT_OK) return rc;
+      for (size_t k = 0; k < W * sampleBuffer.h; k++)
+        if (done_[k].load(std::memory_order_relaxed))
+          sampleBuffer.data[k] = Vector3D(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+      return BDPT_OK;
+    }
     for (const bdpt_tile& t : batch) {
       rgb.resize((size_t)t.w * t.h * 3);
       int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, t.x0, t.y0, t.w, t.h, rgb.data());
@@ -281,10 +294,11 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // Lone pixels merge into rectangles: runs along a row, then equal runs on consecutive rows (an
   // 8x8 cell tile becomes one tile instead of 64 one-pixel blocks). The set of pixels, and so the
   // image, is unchanged.
-  static void coalesce(std::vector<bdpt_tile>& batch) {
+  // Returns whether the batch held lone pixels.
+  static bool coalesce(std::vector<bdpt_tile>& batch) {
     std::vector<bdpt_tile> out, px;
     for (const bdpt_tile& t : batch) (t.w == 1 && t.h == 1 ? px : out).push_back(t);
-    if (px.size() < 2) return;
+    if (px.size() < 2) return !px.empty();
     std::sort(px.begin(), px.end(), [](const bdpt_tile& a, const bdpt_tile& b) {
       return a.y0 != b.y0 ? a.y0 < b.y0 : a.x0 < b.x0;
     });
@@ -304,6 +318,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     }
     out.insert(out.end(), rects.begin(), rects.end());
     batch.swap(out);
+    return true;
   }
 
   void record_failure_locked(const std::string& what) {

@@ -243,6 +243,7 @@ static HDRImageBuffer* load_exr(const char* file_path) {
 
 int main(int argc, char** argv) {
   size_t ns_aa = 1, max_depth = 1, threads = 1, w = 0, h = 0, batch = 32, nal = 1;
+  size_t cx = (size_t)-1, cy = 0, cdx = 0, cdy = 0;   // -p: the cell render (main.cpp:97-103, 180)
   float tol = 0.05f;
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
@@ -250,7 +251,7 @@ int main(int argc, char** argv) {
   bool render = true, uni = false, amd = false, amd_loop = false, tile_loop = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GAB")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GABp:")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -271,6 +272,10 @@ int main(int argc, char** argv) {
       case 'G': amd = true; break;                       // integration check (BDPT_INTEGRATION builds)
       case 'A': amd_loop = true; break;                  // the binding under the reference's own render loop
       case 'B': amd_loop = true; tile_loop = true; break;   // ... its worker loop without the per-tile tonemap
+      case 'p':                                          // main.cpp:97-103
+        cx = atoi(argv[optind - 1]); cy = atoi(argv[optind]); cdx = atoi(argv[optind + 1]); cdy = atoi(argv[optind + 2]);
+        optind += 3;
+        break;
       default: fprintf(stderr, "usage: ref_driver [-s spp] [-t thr] [-m depth] [-r W H] [-f png] [-o npy_prefix] [-j scene.json] [-n] scene.dae\n"); return 1;
     }
   }
@@ -469,7 +474,7 @@ int main(int argc, char** argv) {
   std::chrono::steady_clock::time_point loop_t0 = std::chrono::steady_clock::now();
 #endif
   try {
-    rr->render_to_file(png, (size_t)-1, 0, 0, 0);
+    rr->render_to_file(png, cx, cy, cdx, cdy);   // x = -1: the whole frame
   } catch (const std::exception& e) {   // the binding reports bdpt_* failures as exceptions
     fprintf(stderr, "[ref_driver] %s\n", e.what());
     return 23;

@@ -155,3 +155,37 @@ def test_tile_loop_batches_and_matches_oracle(tmp_path):
     for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
         ours = np.load(f"{prefix}_{name}.npy")
         assert float(np.sqrt(np.mean((ours - ref) ** 2))) < 1e-4, name
+
+
+@needs_bin
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1])
+def test_reference_cell_render_through_binding(tmp_path, threads):
+    """The reference's -p cell branch (render_to_file(x, y, dx, dy) -> raytrace_cell: 8x8 tiles at
+    the cell's corner, raytraced_renderer.cpp:300-318, 622-646) with the binding in place: every
+    pixel is queued alone, the lone pixels of a batch merge into rectangles, every batch refreshes
+    the queued pixels. The PNG (the cell alone) must equal the product CLI's -p render of the same
+    cell and samples; the rate image the reference binary's own. One worker: with several, the
+    reference's own unsynchronised whole-frame write_to_framebuffer calls (:619) race at the end."""
+    from test_output_stage import CLI, read_png
+    W, H, S, M = 64, 48, 64, 5
+    x0, y0, dx, dy = 8, 4, 48, 24
+    png = str(tmp_path / "cell.png")
+    r = subprocess.run([AMD, "-A", "-t", str(threads), "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-p", str(x0),
+                        str(y0), str(dx), str(dy), "-f", png, os.path.join(REPO, "scenes", "CBgems.dae")],
+                       capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Cell job completed" in r.stdout
+    cli = tmp_path / "cli.png"
+    rc = subprocess.run([CLI, "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-p", str(x0), str(y0), str(dx), str(dy),
+                         "-f", str(cli), "--no-stats", os.path.join(REPO, "scenes", "CBgems.dae")],
+                        capture_output=True, text=True, timeout=300)
+    assert rc.returncode == 0, rc.stderr
+    a, b = read_png(png).astype(int), read_png(cli).astype(int)
+    assert a.shape == b.shape == (dy, dx, 4)
+    d = np.abs(a - b)
+    print(f"cell through the binding, -t {threads}: PNG bytes differing {np.count_nonzero(d)} of {d.size}, max {d.max()}")
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
+    key = f"CBgems_{W}x{H}_s{S}_m{M}_cell_{x0}_{y0}_{dx}_{dy}"
+    assert np.array_equal(read_png(str(tmp_path / "cell_rate.png")),
+                          read_png(os.path.join(REPO, "tests", "golden", "png", key + "_rate.png")))

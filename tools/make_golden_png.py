@@ -16,6 +16,9 @@ GOLD = os.path.join(REPO, "tests", "golden")
 DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
 CFGS = [("CBspheres_lambertian", 64, 48, 2, 5), ("CBspheres", 64, 48, 2, 5), ("CBgems", 64, 48, 2, 7),
         ("CBempty", 64, 48, 2, 5)]
+# the -p cell render (render_to_file's cell branch, raytraced_renderer.cpp:622-646): its PNG is the
+# cell alone, its _rate.png the whole frame; 64 spp so the cell image can be compared statistically
+CELLS = [("CBgems", 64, 48, 64, 5, (8, 4, 48, 24))]
 
 
 def main():
@@ -30,6 +33,15 @@ def main():
         ref = np.load(os.path.join(GOLD, "hdr", key + ".npz"))["sample"]
         if not np.array_equal(np.load(pre + "_sample.npy"), ref):
             sys.exit(f"{key}: reference run differs from the committed HDR fixture")
+        shutil.copy(pre + ".png", os.path.join(GOLD, "png", key + ".png"))
+        shutil.copy(pre + "_rate.png", os.path.join(GOLD, "png", key + "_rate.png"))
+        print(key, "ok")
+    for scene, W, H, S, M, (x, y, dx, dy) in CELLS:
+        key = f"{scene}_{W}x{H}_s{S}_m{M}_cell_{x}_{y}_{dx}_{dy}"
+        pre = os.path.join(tmp, key)
+        subprocess.run([DRIVER, "-t", "1", "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-p", str(x), str(y),
+                        str(dx), str(dy), "-f", pre + ".png", os.path.join("/root/reference/dae/sky", scene + ".dae")],
+                       check=True, capture_output=True)
         shutil.copy(pre + ".png", os.path.join(GOLD, "png", key + ".png"))
         shutil.copy(pre + "_rate.png", os.path.join(GOLD, "png", key + "_rate.png"))
         print(key, "ok")
