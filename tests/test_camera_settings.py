@@ -122,7 +122,9 @@ def test_settings_file_lens_replaces_config(tmp_path):
     assert sc.load_camera(_lens_file(tmp_path, 3.25, 0.125), 4.7, 0.0) == (3.25, 0.125)
     sc = B.load_dae(os.path.join(REPO, "scenes", g["scene"] + ".dae"), g["W"], g["H"])
     fd, lr = sc.load_camera(_lens_file(tmp_path, 0, 0, short=True), 4.5, 0.25)
-    assert (fd, lr) in ((4.5, 0.25), (0.0, 0.25))
+    # libstdc++ (GLIBCXX_3.4.30, checked with g++ 11.4 on `istringstream("1 2\n") >> x >> y >> a`):
+    # the sentry fails at EOF before num_get runs, so a stays 4.5
+    assert (fd, lr) == (4.5, 0.25)
 
 
 @pytest.mark.gpu
