@@ -173,11 +173,23 @@ def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads:
     tn = ref_driver_render(dae, W, H, min_spp, M, threads)
     if tn is None:
         return None
-    return {"value": W * H * min_spp / tn / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
+    # also at -t nproc (os.cpu_count(), the whole node) when the box's CPU quota is smaller: the
+    # faster of the two is the baseline, both are reported
+    runs = {threads: tn}
+    if cores["nproc"] > threads:
+        tp = ref_driver_render(dae, W, H, min_spp, M, cores["nproc"])
+        if tp is not None:
+            runs[cores["nproc"]] = tp
+    best = min(runs, key=runs.get)
+    tn = runs[best]
+    return {"value": W * H * min_spp / tn / 1e6, "unit": "Msamples/s", "cores": best, "kind": "reference",
             "host": cores,
+            "threads_tried": {str(t): {"seconds": round(s_, 2), "value": round(W * H * min_spp / s_ / 1e6, 5)}
+                              for t, s_ in runs.items()},
             "sample": f"{name} {W}x{H}, {min_spp} spp, m={M}: the reference's RaytracedRenderer + "
-                      f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2) at -t {threads} "
-                      f"(node nproc {cores['nproc']}, usable {cores['usable']}), {tn:.1f} s of rendering",
+                      f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2), the faster of -t "
+                      f"{' / -t '.join(str(t) for t in runs)} (node nproc {cores['nproc']}, usable "
+                      f"{cores['usable']}): -t {best}, {tn:.1f} s of rendering",
             "spp1": {"value": round(W * H / t1 / 1e6, 5), "seconds": round(t1, 2),
                      "note": "1 spp: the per-tile whole-frame tonemap is a larger share of this time"}}
 
