@@ -497,11 +497,23 @@ class ShardedRender:
     ranks with ONE all-reduce — the only collective (RCCL over xGMI with the "nccl" backend; gloo
     takes device tensors for all_reduce too, which is how two ranks can share one GPU in tests).
     A renderer needs raytrace_tiles(tiles, spp_begin, spp_count) and copy_frame(which, ptr) —
-    BidirectionalPathTracer, or any object with the same two calls."""
+    BidirectionalPathTracer, or any object with the same two calls.
+    With a device `frame`, the renderer's context is put on torch's current stream of that device
+    (set_stream), so the render, the frame copy and the collective (which torch orders after that
+    stream's work) run in order without a host sync; on the null stream reduce() syncs the
+    context before the collective instead."""
 
     def __init__(self, pt, frame, rank: int, world: int, spp: int, scaling: str = "strong", dist=None,
                  group=None):
         self.pt, self.frame = pt, frame
+        self._host_sync = False
+        if getattr(frame, "is_cuda", False) and hasattr(pt, "set_stream"):
+            import torch
+            handle = torch.cuda.current_stream(frame.device).cuda_stream
+            if handle:
+                pt.set_stream(handle)
+            else:   # the null stream: handle 0 would select the context's own stream
+                self._host_sync = True
         self.rank, self.world, self.spp, self.scaling = rank, world, spp, scaling
         self.dist, self.group = dist, group
 
@@ -516,6 +528,8 @@ class ShardedRender:
 
     def reduce(self) -> None:
         self.pt.copy_frame(FRAME_SAMPLE, self.frame.data_ptr())
+        if self._host_sync:
+            self.pt.sync()
         if self.dist is not None and self.world > 1:
             self.dist.all_reduce(self.frame, op=self.dist.ReduceOp.SUM, group=self.group)
 
