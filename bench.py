@@ -143,16 +143,26 @@ def host_cores() -> dict:
     return {"nproc": n, "affinity": aff, "cgroup_quota": quota, "usable": min(x for x in (n, aff, quota) if x)}
 
 
-def ref_driver_render(dae: str, W: int, H: int, spp: int, M: int, threads: int):
+def progress(msg: str) -> None:
+    """a progress line on stderr (the JSON line alone goes to stdout)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def ref_driver_render(dae: str, W: int, H: int, spp: int, M: int, threads: int, timeout: float = 900):
     """Seconds of the reference's own "Rendering... 100%! (Xs)" report (tiles + its per-tile
     whole-frame tonemap, raytraced_renderer.cpp:595-620,654-682; its timer starts after
     build_accel), or None."""
     import re
     import tempfile
+    progress(f"reference CPU path: {os.path.basename(dae)} {W}x{H} s{spp} m{M} -t {threads}")
     with tempfile.TemporaryDirectory() as td:
-        r = subprocess.run([REF_DRIVER, "-s", str(spp), "-t", str(threads), "-m", str(M), "-r", str(W), str(H),
-                            "-f", os.path.join(td, "ref.png"), os.path.abspath(dae)],
-                           capture_output=True, text=True, timeout=900, cwd=td)
+        try:
+            r = subprocess.run([REF_DRIVER, "-s", str(spp), "-t", str(threads), "-m", str(M), "-r", str(W), str(H),
+                                "-f", os.path.join(td, "ref.png"), os.path.abspath(dae)],
+                               capture_output=True, text=True, timeout=timeout, cwd=td)
+        except subprocess.TimeoutExpired:
+            progress(f"reference CPU path at -t {threads}: over {timeout:.0f} s, not counted")
+            return None
     m = re.findall(r"Rendering\.\.\. 100%! \(([0-9.]+)s\)", r.stdout)
     return float(m[-1]) if r.returncode == 0 and m else None
 
@@ -177,7 +187,7 @@ def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads:
     # faster of the two is the baseline, both are reported
     runs = {threads: tn}
     if cores["nproc"] > threads:
-        tp = ref_driver_render(dae, W, H, min_spp, M, cores["nproc"])
+        tp = ref_driver_render(dae, W, H, min_spp, M, cores["nproc"], timeout=max(60.0, 2.0 * tn))
         if tp is not None:
             runs[cores["nproc"]] = tp
     best = min(runs, key=runs.get)
@@ -491,9 +501,12 @@ def main() -> int:
         out["config"]["integrator"] = "PathTracer (pathtracer.cpp:47-340)"
     cores = host_cores()
     thr = cores["usable"]
+    progress(f"timed {args.steps} steps: {value:.1f} Msamples/s")
     if world == 1 and not args.no_parity and not use_pt:
+        progress("parity leg: GPU vs oracle modes 2 and 1")
         out["parity"] = parity_check(scene, W, H, M, seed, rr=rr, threads=thr)
     if world == 1 and not args.no_cpu_baseline and not use_pt:
+        progress("CPU baseline: oracle port")
         port = cpu_baseline(scene, os.path.basename(scene_path), W, H, SPP, M, threads=thr, rr=rr)
         # the reference cannot run the environment light / roulette under BDPT: port only
         ref = (None if (env_desc or rr)
