@@ -185,20 +185,23 @@ def cpu_baseline_reference(dae: str, name: str, W: int, H: int, M: int, threads:
         return None
     # also at -t nproc (os.cpu_count(), the whole node) when the box's CPU quota is smaller: the
     # faster of the two is the baseline, both are reported
-    runs = {threads: tn}
+    runs, slow = {threads: tn}, {}
     if cores["nproc"] > threads:
-        tp = ref_driver_render(dae, W, H, min_spp, M, cores["nproc"], timeout=max(60.0, 2.0 * tn))
+        cap = max(60.0, 2.0 * tn)
+        tp = ref_driver_render(dae, W, H, min_spp, M, cores["nproc"], timeout=cap)
         if tp is not None:
             runs[cores["nproc"]] = tp
+        else:
+            slow[str(cores["nproc"])] = {"seconds": None, "note": f"stopped after {cap:.0f} s wall (over 2x -t {threads})"}
     best = min(runs, key=runs.get)
     tn = runs[best]
     return {"value": W * H * min_spp / tn / 1e6, "unit": "Msamples/s", "cores": best, "kind": "reference",
             "host": cores,
-            "threads_tried": {str(t): {"seconds": round(s_, 2), "value": round(W * H * min_spp / s_ / 1e6, 5)}
-                              for t, s_ in runs.items()},
+            "threads_tried": {**{str(t): {"seconds": round(s_, 2), "value": round(W * H * min_spp / s_ / 1e6, 5)}
+                                 for t, s_ in runs.items()}, **slow},
             "sample": f"{name} {W}x{H}, {min_spp} spp, m={M}: the reference's RaytracedRenderer + "
                       f"BidirectionalPathTracer (oracle/_ref/ref_driver, -O3 -mavx2), the faster of -t "
-                      f"{' / -t '.join(str(t) for t in runs)} (node nproc {cores['nproc']}, usable "
+                      f"{' / -t '.join([str(t) for t in runs] + list(slow))} (node nproc {cores['nproc']}, usable "
                       f"{cores['usable']}): -t {best}, {tn:.1f} s of rendering",
             "spp1": {"value": round(W * H / t1 / 1e6, 5), "seconds": round(t1, 2),
                      "note": "1 spp: the per-tile whole-frame tonemap is a larger share of this time"}}
