@@ -35,6 +35,8 @@ RENDERS = [
     ("CBempty", 64, 48, 2, 5, True),
     ("CBspheres", 160, 120, 1, 5, False),
     ("CBspheres_lambertian", 480, 360, 1, 5, False),
+    # BASELINE.json configs[0] itself: CBspheres_lambertian 480x360 -s 4 -m 5 at -t 1
+    ("CBspheres_lambertian", 480, 360, 4, 5, False),
     ("CBspheres", 480, 360, 1, 5, False),
     ("CBgems", 240, 180, 1, 7, False),
     ("CBspheres", 96, 72, 3, 1, False),
