@@ -329,7 +329,9 @@ def main() -> int:
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) the process group is made at every world size, 1 included, so
+    # the RCCL all-reduce of the frame runs on one GPU exactly as it does on eight
+    if world > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -456,7 +458,8 @@ def main() -> int:
                    + (" unidirectional PathTracer" if use_pt else "")
                    + (", whole frame per step split across GPUs" if scaling == "strong" else ", full spp per GPU")
                    + (" (row bands)" if use_pt else " (sample ranges)")
-                   + (" + RCCL all-reduce" if args.dist_backend == "nccl" else " + gloo all-reduce"),
+                   + ("" if dist is None else " + RCCL all-reduce" if args.dist_backend == "nccl"
+                      else " + gloo all-reduce"),
                    "workload_key": args.workload if named else "custom",
                    "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
                    "scene": os.path.relpath(scene_path, REPO), "width": W, "height": H, "spp": SPP,
@@ -495,7 +498,7 @@ def main() -> int:
     }
     if traffic_info:
         out["roofline"]["traffic_pmc"] = traffic_info
-    if world > 1:
+    if dist is not None:
         out["per_rank"] = {"elapsed_s": [round(x, 4) for x in rank_elapsed],
                            "kernel_ms": [round(x, 3) for x in rank_kern],
                            "samples_per_step": [int(r[2]) for r in rows], "device": [int(r[3]) for r in rows],

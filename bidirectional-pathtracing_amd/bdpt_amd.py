@@ -336,6 +336,11 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
                                   C.POINTER(C.POINTER(C.c_float))]
     lib.bdpt_exr_free.argtypes = [C.POINTER(C.c_float)]
     lib.bdpt_exr_free.restype = None
+    lib.bdpt_reduce_create.argtypes = [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bdpt_reduce_frames.argtypes = [C.c_void_p, C.c_int32]
+    lib.bdpt_reduce_ranks.argtypes = [C.c_void_p]
+    lib.bdpt_reduce_destroy.argtypes = [C.c_void_p]
+    lib.bdpt_reduce_destroy.restype = None
     if path is None:
         _lib = lib
     return lib
@@ -472,6 +477,41 @@ class PathTracer(BidirectionalPathTracer):
                                   lens_radius=lens_radius, focal_distance=focal_distance))
 
 
+class FrameReducer:
+    """The C-ABI's multi-GPU frame reduce (bdpt_reduce_*, ABI v9) over renderers in ONE process —
+    the CLI's -g N: one RCCL communicator clique over their distinct devices (contexts sharing a
+    device are summed on it first), and per reduce(root) one grouped ncclReduce of every
+    renderer's eye and light frames into the root renderer's. Afterwards root.read_frame() is the
+    whole image; the others' frames are unchanged."""
+
+    def __init__(self, renderers: Sequence["BidirectionalPathTracer"]):
+        self.lib = load_library()
+        self.renderers = list(renderers)   # the contexts must outlive the reducer
+        arr = (C.c_void_p * len(self.renderers))(*[r.ctx.value for r in self.renderers])
+        h = C.c_void_p()
+        _check(self.lib.bdpt_reduce_create(arr, len(self.renderers), C.byref(h)), self.lib)
+        self.h = h
+
+    @property
+    def ranks(self) -> int:
+        """RCCL ranks of the communicator (distinct devices)"""
+        return int(self.lib.bdpt_reduce_ranks(self.h))
+
+    def reduce(self, root: int = 0) -> None:
+        _check(self.lib.bdpt_reduce_frames(self.h, root), self.lib)
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.bdpt_reduce_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # --- multi-GPU: one process per GPU under torch.distributed (SURVEY.md §8e, DESIGN.md §6) ---------
 # Pixel-samples are independent except the t = 1 light-tracing splats, which land anywhere
 # (bidirection.cpp:457-466), so a frame cannot be split into tiles and gathered: the ranks split
@@ -530,7 +570,7 @@ class ShardedRender:
         self.pt.copy_frame(FRAME_SAMPLE, self.frame.data_ptr())
         if self._host_sync:
             self.pt.sync()
-        if self.dist is not None and self.world > 1:
+        if self.dist is not None:   # at world size 1 too: the same RCCL call on one rank
             self.dist.all_reduce(self.frame, op=self.dist.ReduceOp.SUM, group=self.group)
 
     def step(self, step: int) -> None:
@@ -544,6 +584,6 @@ class ShardedRender:
         v = torch.zeros(self.world, len(values), dtype=torch.float64,
                         device=device if device is not None else self.frame.device)
         v[self.rank] = torch.tensor(values, dtype=torch.float64)
-        if self.dist is not None and self.world > 1:
+        if self.dist is not None:
             self.dist.all_reduce(v, op=self.dist.ReduceOp.SUM, group=self.group)
         return [[float(x) for x in row] for row in v.cpu()]

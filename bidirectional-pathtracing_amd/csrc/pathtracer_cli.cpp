@@ -7,14 +7,15 @@
 //
 // Same flags and defaults as the reference (-s 1, -m 1, 800x600 when -r is absent; -t / -l are
 // accepted and do not apply to the GPU path; -p renders one cell). -g N splits the sample range
-// over N devices (one context and one host thread per device) and sums the frames. -e loads an
+// over N devices (one context and one host thread per device) and sums the frames on the devices with
+// one RCCL reduce into device 0's (bdpt_reduce_frames, inside the timed region). -e loads an
 // environment map as the reference's -e does (load_exr, main.cpp:115-119) — under BDPT, which the
 // reference cannot run with it; --rr turns on Russian roulette (bidirection.cpp:87-93).
 // --pt selects the reference's unidirectional PathTracer (pathtracer.cpp:47-340) with its flags
 // -l, -a, -H, -b, -d (main.cpp:107-141); its -g N splits the frame into row bands (whole pixels).
 // Output: the tonemapped PNG and the "_rate.png" sampling-rate image, as render_to_file writes
 // them (raytraced_renderer.cpp:330-347, 690-761). The "Rendering... 100%! (Xs)" time covers the
-// production kernel's render and the frame read-back; bdpt_create (BVH build + upload) runs before
+// production kernel's render, the frame reduce and the frame read-back; bdpt_create (BVH build + upload) runs before
 // the timer starts, as the reference's starts after build_accel. The report's ray / test counts
 // come from a second, untimed render of the same samples by the instrumented kernel (--no-stats
 // skips it).
@@ -159,9 +160,7 @@ int main(int argc, char** argv) {
 
   std::vector<bdpt_tile> tiles;
   if (cx >= 0) tiles.push_back(bdpt_tile{(int32_t)cx, (int32_t)cy, (int32_t)cdx, (int32_t)cdy});
-  std::vector<std::vector<float>> frames(gpus, std::vector<float>((size_t)w * h * 3, 0.0f));
   std::vector<int> rcs(gpus, 0);
-  std::vector<std::vector<int32_t>> counts(gpus, std::vector<int32_t>((size_t)w * h, 0));
   std::vector<std::string> errs(gpus);
   std::vector<bdpt_stats> st(gpus);
   std::vector<void*> ctxs(gpus, nullptr);
@@ -206,8 +205,6 @@ int main(int argc, char** argv) {
         } else if (phase == 1) {
           if (s1[g] > s0[g])
             rc = bdpt_render(ctxs[g], mine[g].empty() ? nullptr : mine[g].data(), (int32_t)mine[g].size(), s0[g], s1[g] - s0[g]);
-          if (rc == BDPT_OK) rc = bdpt_read_frame(ctxs[g], BDPT_FRAME_SAMPLE, frames[g].data());
-          if (rc == BDPT_OK) rc = bdpt_read_sample_counts(ctxs[g], counts[g].data());
         } else {
           bdpt_params p = params(g, true);
           void* sc = nullptr;
@@ -229,20 +226,36 @@ int main(int argc, char** argv) {
       }
     return true;
   };
+  bdpt_reducer* red = nullptr;
+  auto release = [&] {   // the render contexts, before the stats pass creates its own
+    bdpt_reduce_destroy(red);
+    red = nullptr;
+    for (void*& c : ctxs)
+      if (c) { bdpt_destroy(c); c = nullptr; }
+  };
   auto cleanup = [&] {
-    for (void* c : ctxs)
-      if (c) bdpt_destroy(c);
+    release();
     bdpt_dae_free(dae);
     bdpt_exr_free(env_rgb);
   };
   if (!run(0)) { cleanup(); return 1; }
+  // the frame reduce over the N contexts (RCCL, bdpt_reduce_*): its communicator is set up here,
+  // outside the timer like the contexts; the reduce itself runs inside it
+  if (bdpt_reduce_create(ctxs.data(), gpus, &red) != BDPT_OK) { fail("creating the frame reduce"); cleanup(); return 1; }
+  std::vector<float> img((size_t)w * h * 3, 0.0f);
+  std::vector<int32_t> count((size_t)w * h, 0);
   auto t0 = std::chrono::steady_clock::now();
   if (!run(1)) { cleanup(); return 1; }
+  // every device's partial frame summed into context 0's over xGMI, then one read-back
+  if (bdpt_reduce_frames(red, 0) != BDPT_OK || bdpt_read_frame(ctxs[0], BDPT_FRAME_SAMPLE, img.data()) != BDPT_OK ||
+      bdpt_read_sample_counts(ctxs[0], count.data()) != BDPT_OK) {
+    fail("reducing the frames");
+    cleanup();
+    return 1;
+  }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  release();
   if (stats && !run(2)) { cleanup(); return 1; }
-  std::vector<float>& img = frames[0];
-  for (int g = 1; g < gpus; g++)
-    for (size_t k = 0; k < img.size(); k++) img[k] += frames[g][k];
   const double samples = (double)(tiles.empty() ? (long long)w * h : cdx * cdy) * spp;
   // the reference's end-of-render report (raytraced_renderer.cpp:679-682), on stdout: time, rays
   // traced (closest-hit walk rays + connection rays), Mrays/s, primitive tests per ray
@@ -278,11 +291,7 @@ int main(int argc, char** argv) {
   fprintf(stderr, "Done!\n");
   std::vector<float> rate((size_t)w * h, 0.0f);
   if (pt) {   // sampleCountBuffer[k] * 1.0f / ns_aa (save_sampling_rate_image, raytraced_renderer.cpp:737)
-    for (size_t k = 0; k < rate.size(); k++) {
-      int32_t n = 0;
-      for (int g = 0; g < gpus; g++) n += counts[g][k];
-      rate[k] = n * 1.0f / spp;
-    }
+    for (size_t k = 0; k < rate.size(); k++) rate[k] = count[k] * 1.0f / spp;   // summed by the reduce
   } else if (tiles.empty()) {
     std::fill(rate.begin(), rate.end(), 1.0f);   // every pixel got ns_aa samples (bidirection.cpp:539)
   } else {

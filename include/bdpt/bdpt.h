@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BDPT_ABI_VERSION 8
+#define BDPT_ABI_VERSION 9
 
 enum bdpt_status {
   BDPT_OK = 0,
@@ -237,6 +237,27 @@ int bdpt_frame_device_ptr(void* ctx, int32_t which, void** dptr);
 int bdpt_copy_frame(void* ctx, int32_t which, void* dst_device);
 
 int bdpt_get_stats(void* ctx, bdpt_stats* out);
+
+/* ABI v9: the multi-GPU frame reduce. The reference renders with N CPU threads
+ * into one shared frame (raytraced_renderer.cpp:325-327); here N contexts — one per GPU, each
+ * rendering its own sample range of every pixel — hold partial W*H*3 frames, and because the t = 1
+ * light splats land on any pixel (bidirection.cpp:457-466) the image is their whole-frame sum.
+ * bdpt_reduce_create builds one RCCL communicator clique over the contexts' distinct devices
+ * (ncclCommInitAll; contexts sharing a device are summed on it first). bdpt_reduce_frames then
+ * enqueues one grouped ncclReduce (sum, fp32) of every context's eye and light frames into the
+ * `root` context's frames, on the contexts' streams (under the PathTracer the sampleCountBuffer is
+ * summed too); afterwards bdpt_read_frame(root, ...) returns the whole image. The other contexts'
+ * frames are unchanged. Async; later work on any listed ctx is ordered after it. The contexts must
+ * outlive the reducer and share the frame size and integrator. RCCL is loaded on first use
+ * (librccl.so.1); without it these calls fail with BDPT_E_DEVICE. */
+typedef struct bdpt_reducer bdpt_reducer;
+int bdpt_reduce_create(void* const* ctxs, int32_t n, bdpt_reducer** out);
+int bdpt_reduce_frames(bdpt_reducer* r, int32_t root);
+/* RCCL ranks of the reducer's communicator (= distinct devices), or BDPT_E_INVALID. */
+int bdpt_reduce_ranks(const bdpt_reducer* r);
+/* ncclGetVersion of the RCCL that the reducer uses (loads it), or a negative BDPT_E_* code. */
+int bdpt_reduce_rccl_version(void);
+void bdpt_reduce_destroy(bdpt_reducer* r);
 
 /* Test hook: closest-hit / any-hit queries for a batch of rays through the device BVH
  * (BVHAccel::intersect, bvh.cpp:161-188). rays: n*8 floats {o.xyz, d.xyz, min_t, max_t};

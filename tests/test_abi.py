@@ -31,7 +31,23 @@ def test_library_exports_every_declared_function():
 
 
 def test_abi_version():
-    assert B.load_library().bdpt_abi_version() == 8   # v2: envmap + RR; v3: integrator; v4: LDS stats; v5: camera settings; v6: env-table stats; v7: camera lens settings; v8: frame rectangles
+    assert B.load_library().bdpt_abi_version() == 9   # v2: envmap + RR; v3: integrator; v4: LDS stats; v5: camera settings; v6: env-table stats; v7: camera lens settings; v8: frame rectangles; v9: RCCL frame reduce
+
+
+def test_frame_reduce_loads_rccl_and_validates_arguments():
+    """bdpt_reduce_*: the product loads RCCL itself (dlopen librccl.so.1, no GPU needed for
+    ncclGetVersion), and rejects bad arguments before touching a device."""
+    lib = B.load_library()
+    v = lib.bdpt_reduce_rccl_version()
+    assert v >= 20000, lib.bdpt_last_error()   # NCCL_VERSION_CODE of RCCL 2.x
+    h = C.c_void_p()
+    assert lib.bdpt_reduce_create(None, 1, C.byref(h)) == B.BDPT_E_INVALID
+    arr = (C.c_void_p * 1)(None)
+    assert lib.bdpt_reduce_create(arr, 0, C.byref(h)) == B.BDPT_E_INVALID
+    assert lib.bdpt_reduce_create(arr, 1, C.byref(h)) == B.BDPT_E_INVALID and not h.value
+    assert lib.bdpt_reduce_frames(None, 0) == B.BDPT_E_INVALID
+    assert lib.bdpt_reduce_ranks(None) == B.BDPT_E_INVALID
+    lib.bdpt_reduce_destroy(None)
 
 
 def test_null_arguments_rejected():

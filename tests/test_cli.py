@@ -132,8 +132,10 @@ def test_cli_pathtracer(tmp_path, scene):
 @pytest.mark.parametrize("gpus,spp", [(2, 2), (3, 4)])
 def test_cli_multi_gpu_split(tmp_path, gpus, spp):
     """-g N: the sample range split over N workers (one context and one host thread each) and the
-    frames summed on the host. --devices puts every worker on device 0 so a one-GPU box runs the
-    N-worker path; the image must match one render of all samples (oracle mode 2)."""
+    frames summed by the C-ABI's reduce (bdpt_reduce_frames: on-device sum of the contexts sharing a
+    GPU, then the RCCL ncclReduce, inside the timed region). --devices puts every worker on device 0
+    so a one-GPU box runs the N-worker path; the image must match one render of all samples (oracle
+    mode 2). (-g 1, test_cli_renders_scene_like_oracle, goes through a one-rank RCCL reduce.)"""
     W, H, M = 64, 48, 5
     out = tmp_path / "g.png"
     r = subprocess.run([CLI, "-s", str(spp), "-m", str(M), "-r", str(W), str(H), "-g", str(gpus), "--devices",
