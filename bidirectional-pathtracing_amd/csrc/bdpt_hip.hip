@@ -597,6 +597,9 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr int kFlatMaxPrims = 24;   // flat leaf list up to this many primitives; measured: CBspheres 488 -> 511 Msamples/s, CBspheres_lambertian +6%, CBempty -1%
 constexpr size_t kBlocksPerCu = 4 * kMinWaves / kWavesPerBlock;
 constexpr size_t kLdsSceneMax = kLdsPerCu / kBlocksPerCu - kWavesPerBlock * sizeof(WaveQ) - 256 - kStaticLds;
+// LM 2's treelet gets kLdsSceneMax - kLdsStackBytes (an unsigned difference): it must hold at least
+// one node, or the subtraction wraps and the treelet size is no longer capped by the LDS budget
+static_assert(kLdsSceneMax > kLdsStackBytes + (size_t)node_bytes(lm_width(2)), "LDS budget: wave queues + stack slots leave no treelet");
 
 // Persistent launch: as many blocks as are co-resident (occupancy query with this launch's LDS),
 // never more waves than work items.

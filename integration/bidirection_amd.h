@@ -25,11 +25,17 @@
 //     whole frame — light-tracing splats land anywhere (bidirection.cpp:457-466) — into
 //     sampleBuffer / eyeBuffer / lightBuffer, so the last write_to_framebuffer and save_image see
 //     the final image.
-// A pixel that no 32x32 tile covers (the -p cell path, 8x8 tiles at an arbitrary corner,
-// :300-318) is queued alone; lone pixels of a batch merge into rectangles, and their call returns
-// once its batch is in sampleBuffer (the cell render copies frameBuffer as soon as the workers
-// end, :640-645). attach() / raytrace_tile() / raytrace_frame() / finish() remain for callers that
-// drive whole tiles or frames themselves.
+// The -p cell path (8x8 tiles from the cell's corner, :300-318) cannot be told apart from a tile
+// loop by the pixels alone: a cell may hold a 32-aligned pixel, which would queue a whole 32x32
+// tile past the cell's edge. A host that renders cells names the cell first — set_cell(x, y, dx,
+// dy), the one line a maintainer adds to render_to_file's cell branch (:338-345, next to cell_tl /
+// cell_br) — and the frame's first cell pixel then queues the whole cell as one rectangle: one
+// launch, one copy of the cell's pixels, and every worker returns only once the cell is in
+// sampleBuffer (the cell render copies frameBuffer as soon as the workers end, :640-645). Without
+// it, a pixel that no 32x32 tile covers is queued alone; lone pixels of a batch merge into
+// rectangles, and their call returns once its batch (and every pixel queued before it, refreshed
+// within their bounding box) is in sampleBuffer. attach() / raytrace_tile() / raytrace_frame() /
+// finish() remain for callers that drive whole tiles or frames themselves.
 //
 // Flattening reads the reference's scene objects: Triangle p1..p3 / n1..n3, Sphere o / r, the
 // BSDF parameters, the light fields and the camera (hFov, vFov, nClip, fClip, pos, c2w, w2c). The
@@ -50,6 +56,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdint>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -189,6 +196,18 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       record_failure_locked(e.what());
     }
   }
+  // The -p cell (render_to_file's cell branch, raytraced_renderer.cpp:338-345): the rectangle
+  // [x, x+dx) x [y, y+dy) that the coming frames' raytrace_pixel calls cover (kept across clear()
+  // and set_frame_size(), which start_raytracing runs first); clear_cell() returns to whole frames.
+  void set_cell(size_t x, size_t y, size_t dx, size_t dy) {
+    std::lock_guard<std::mutex> lk(mu_);
+    cell_ = bdpt_tile{(int32_t)x, (int32_t)y, (int32_t)dx, (int32_t)dy};
+    has_cell_ = dx > 0 && dy > 0;
+  }
+  void clear_cell() {
+    std::lock_guard<std::mutex> lk(mu_);
+    has_cell_ = false;
+  }
   // empty, or the first failure of the frame's raytrace_pixel calls
   std::string error() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -200,7 +219,8 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   double device_seconds() { std::lock_guard<std::mutex> lk(mu_); return busy_s_; }
 
  private:
-  // Queues the tile whose first pixel (x, y) is — tiles start at multiples of imageTileSize = 32,
+  // Queues the whole cell when one is set (set_cell; returns true: the caller waits for it), else
+  // the tile whose first pixel (x, y) is — tiles start at multiples of imageTileSize = 32,
   // raytraced_renderer.cpp:83,293-298 — or else the pixel alone (returns true then). mu_ held.
   bool enqueue_locked(size_t x, size_t y, size_t W, size_t H) {
     if (!ctx_) {
@@ -214,16 +234,31 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       check(attach(prims, scene->lights, *camera, env));
     }
     if (done_[x + y * W].load(std::memory_order_relaxed)) return false;
-    const bool corner = x % kTile == 0 && y % kTile == 0;
-    const size_t tw = corner ? std::min(kTile, W - x) : 1, th = corner ? std::min(kTile, H - y) : 1;
-    for (size_t yy = y; yy < y + th; yy++)
-      for (size_t xx = x; xx < x + tw; xx++) {
+    size_t x0 = x, y0 = y, tw = 1, th = 1;
+    bool wait = true;
+    if (has_cell_ && (int64_t)x >= cell_.x0 && (int64_t)x < (int64_t)cell_.x0 + cell_.w && (int64_t)y >= cell_.y0 &&
+        (int64_t)y < (int64_t)cell_.y0 + cell_.h) {
+      // the cell, clipped to the frame, as one rectangle
+      x0 = (size_t)std::max<int64_t>(0, cell_.x0);
+      y0 = (size_t)std::max<int64_t>(0, cell_.y0);
+      tw = (size_t)std::min<int64_t>((int64_t)W, (int64_t)cell_.x0 + cell_.w) - x0;
+      th = (size_t)std::min<int64_t>((int64_t)H, (int64_t)cell_.y0 + cell_.h) - y0;
+    } else if (!has_cell_ && x % kTile == 0 && y % kTile == 0) {
+      tw = std::min(kTile, W - x);
+      th = std::min(kTile, H - y);
+      wait = false;
+    }
+    for (size_t yy = y0; yy < y0 + th; yy++)
+      for (size_t xx = x0; xx < x0 + tw; xx++) {
         sampleCountBuffer[xx + yy * W] = ns_aa;   // bidirection.cpp:539
         if (!done_[xx + yy * W].exchange(1, std::memory_order_release)) queued_++;
       }
-    pending_.push_back(bdpt_tile{(int32_t)x, (int32_t)y, (int32_t)tw, (int32_t)th});
+    // the bounding box of everything queued this frame: what a lone batch refreshes
+    qx0_ = std::min(qx0_, x0); qy0_ = std::min(qy0_, y0);
+    qx1_ = std::max(qx1_, x0 + tw); qy1_ = std::max(qy1_, y0 + th);
+    pending_.push_back(bdpt_tile{(int32_t)x0, (int32_t)y0, (int32_t)tw, (int32_t)th});
     seq_++;
-    return !corner;
+    return wait;
   }
 
   // Launches the queued tiles in batches. The caller that finds no launch in flight becomes the
@@ -241,16 +276,25 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       // into sampleBuffer is skipped (only its completion is waited for)
       const bool last = queued_ == sampleBuffer.w * sampleBuffer.h;
       const bool lone = coalesce(batch);
+      const bdpt_tile box = {(int32_t)qx0_, (int32_t)qy0_, (int32_t)(qx1_ - qx0_), (int32_t)(qy1_ - qy0_)};
       lk.unlock();
       const auto t0 = std::chrono::steady_clock::now();
-      int rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
-      if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch, lone);   // waits for the launch
+      int rc = BDPT_E_INVALID;
+      std::string what;
+      try {   // nothing may leave this section with mu_ released (and launching_ still set)
+        rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
+        if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch, lone, box);   // waits for the launch
+        if (rc != BDPT_OK) what = bdpt_last_error();
+      } catch (const std::exception& e) {
+        what = e.what();
+        rc = BDPT_E_INVALID;
+      }
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       lk.lock();
       launches_++;
       busy_s_ += dt;
       copied_ = upto;
-      if (rc != BDPT_OK) record_failure_locked(bdpt_last_error());
+      if (rc != BDPT_OK) record_failure_locked(what);
       cv_.notify_all();
     }
     launching_ = false;
@@ -261,21 +305,25 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // (more than 16: the workers queued faster than the device rendered, as without the reference's
   // per-tile tonemap) is not copied: finish() brings the whole frame in when the last pixel is
   // queued, and the copy would only delay the next launch. A batch with lone pixels (their
-  // callers wait for them, -p cell path) refreshes every queued pixel.
-  int copy_back(const std::vector<bdpt_tile>& batch, bool lone) {
+  // callers wait for them, the -p cell path without set_cell) refreshes every queued pixel, read
+  // as one rectangle: `box`, the bounding box of what the frame has queued.
+  int copy_back(const std::vector<bdpt_tile>& batch, bool lone, const bdpt_tile& box) {
     if (batch.size() > 16 && !lone) return bdpt_sync(ctx_);
     const size_t W = sampleBuffer.w;
     std::vector<float> rgb;
     if (lone) {
-      // The -p cell path never queues the whole frame, so finish() never runs: every batch
-      // refreshes all pixels queued so far, so the splats of later samples (bidirection.cpp:
-      // 457-466) reach the cell's earlier pixels too, and the cell's last batch leaves it complete.
-      rgb.resize(W * sampleBuffer.h * 3);
-      int rc = bdpt_read_frame(ctx_, BDPT_FRAME_SAMPLE, rgb.data());
+      // The cell path never queues the whole frame, so finish() never runs: every batch refreshes
+      // all pixels queued so far, so the splats of later samples (bidirection.cpp:457-466) reach
+      // the cell's earlier pixels too, and the cell's last batch leaves it complete.
+      rgb.resize((size_t)box.w * box.h * 3);
+      int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, box.x0, box.y0, box.w, box.h, rgb.data());
       if (rc != BDPT_OK) return rc;
-      for (size_t k = 0; k < W * sampleBuffer.h; k++)
-        if (done_[k].load(std::memory_order_relaxed))
-          sampleBuffer.data[k] = Vector3D(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+      for (int32_t yy = 0; yy < box.h; yy++)
+        for (int32_t xx = 0; xx < box.w; xx++) {
+          const size_t k = (size_t)(box.x0 + xx) + (size_t)(box.y0 + yy) * W;
+          const float* v = &rgb[3 * ((size_t)xx + (size_t)yy * box.w)];
+          if (done_[k].load(std::memory_order_relaxed)) sampleBuffer.data[k] = Vector3D(v[0], v[1], v[2]);
+        }
       return BDPT_OK;
     }
     for (const bdpt_tile& t : batch) {
@@ -410,6 +458,8 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     const size_t n = sampleBuffer.w * sampleBuffer.h;
     done_.reset(n ? new std::atomic<uint8_t>[n]() : nullptr);   // value-initialised: all 0
     pending_.clear();
+    qx0_ = qy0_ = SIZE_MAX;
+    qx1_ = qy1_ = 0;
     queued_ = seq_ = copied_ = launches_ = 0;
     busy_s_ = 0.0;
     launching_ = finished_ = false;
@@ -438,6 +488,9 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   std::unique_ptr<std::atomic<uint8_t>[]> done_;   // per pixel: queued (with its tile)
   std::vector<bdpt_tile> pending_;                 // queued, not yet launched
   size_t queued_ = 0;                              // pixels queued this frame
+  size_t qx0_ = SIZE_MAX, qy0_ = SIZE_MAX, qx1_ = 0, qy1_ = 0;   // their bounding box
+  bdpt_tile cell_ = {0, 0, 0, 0};                  // set_cell: the -p cell, kept across frames
+  bool has_cell_ = false;
   size_t seq_ = 0, copied_ = 0;                    // tiles queued / tiles whose batch is in sampleBuffer
   size_t launches_ = 0;
   double busy_s_ = 0.0;

@@ -248,10 +248,10 @@ int main(int argc, char** argv) {
   bool hemi = false;
   double lens = 0.0, focal = 4.7;
   std::string png = "/dev/null", npy_prefix, scene_json, cam_settings;
-  bool render = true, uni = false, amd = false, amd_loop = false, tile_loop = false;
+  bool render = true, uni = false, amd = false, amd_loop = false, tile_loop = false, no_cell_hook = false;
   HDRImageBuffer* envmap = nullptr;
   int opt;
-  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GABp:")) != -1) {
+  while ((opt = getopt(argc, argv, "s:t:m:r:f:o:j:ne:Ua:Hb:d:l:c:GABCp:")) != -1) {
     switch (opt) {
       case 's': ns_aa = atoi(optarg); break;
       case 't': threads = atoi(optarg); break;
@@ -272,6 +272,7 @@ int main(int argc, char** argv) {
       case 'G': amd = true; break;                       // integration check (BDPT_INTEGRATION builds)
       case 'A': amd_loop = true; break;                  // the binding under the reference's own render loop
       case 'B': amd_loop = true; tile_loop = true; break;   // ... its worker loop without the per-tile tonemap
+      case 'C': no_cell_hook = true; break;              // -A -p without the binding's set_cell line
       case 'p':                                          // main.cpp:97-103
         cx = atoi(argv[optind - 1]); cy = atoi(argv[optind]); cdx = atoi(argv[optind + 1]); cdy = atoi(argv[optind + 2]);
         optind += 3;
@@ -472,6 +473,11 @@ int main(int argc, char** argv) {
     return 0;
   }
   std::chrono::steady_clock::time_point loop_t0 = std::chrono::steady_clock::now();
+#endif
+#ifdef BDPT_INTEGRATION
+  // the maintainer's second line, for -p cell renders: render_to_file's cell branch
+  // (raytraced_renderer.cpp:338-345) names the cell to the binding next to cell_tl / cell_br
+  if (amd_pt && cx != (size_t)-1 && !no_cell_hook) amd_pt->set_cell(cx, cy, cdx, cdy);
 #endif
   try {
     rr->render_to_file(png, cx, cy, cdx, cdy);   // x = -1: the whole frame

@@ -51,7 +51,8 @@ def test_cli_renders_scene_like_oracle(tmp_path):
     assert os.path.exists(tmp_path / "cbs_rate.png")
 
 
-def test_cli_cell_render(tmp_path):
+@pytest.mark.parametrize("cell", [(8, 4, 48, 24), (16, 12, 40, 28)])
+def test_cli_cell_render(tmp_path, cell):
     """-p x y dx dy renders one cell (RaytracedRenderer::render_to_file's cell branch,
     raytraced_renderer.cpp:622-646): the PNG is the cell alone (dx x dy, as raytrace_cell copies it
     out of the frame buffer and save_image writes that buffer), the _rate.png the whole frame with
@@ -61,7 +62,7 @@ def test_cli_cell_render(tmp_path):
     flipped cell decorrelates: measured 0.49 vs 0.20 with the CPU build of the device code) and of
     the same mean brightness."""
     W, H, S, M = 64, 48, 64, 5
-    x0, y0, dx, dy = 8, 4, 48, 24
+    x0, y0, dx, dy = cell
     key = f"CBgems_{W}x{H}_s{S}_m{M}_cell_{x0}_{y0}_{dx}_{dy}"
     out = tmp_path / "cell.png"
     r = subprocess.run([CLI, "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-p", str(x0), str(y0), str(dx), str(dy),

@@ -159,19 +159,26 @@ def test_tile_loop_batches_and_matches_oracle(tmp_path):
 
 @needs_bin
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1])
-def test_reference_cell_render_through_binding(tmp_path, threads):
+@pytest.mark.parametrize("threads,cell,hook", [(1, (8, 4, 48, 24), True), (1, (16, 12, 40, 28), True),
+                                               (1, (8, 4, 48, 24), False)])
+def test_reference_cell_render_through_binding(tmp_path, threads, cell, hook):
     """The reference's -p cell branch (render_to_file(x, y, dx, dy) -> raytrace_cell: 8x8 tiles at
-    the cell's corner, raytraced_renderer.cpp:300-318, 622-646) with the binding in place: every
-    pixel is queued alone, the lone pixels of a batch merge into rectangles, every batch refreshes
-    the queued pixels. The PNG (the cell alone) must equal the product CLI's -p render of the same
-    cell and samples; the rate image the reference binary's own. One worker: with several, the
-    reference's own unsynchronised whole-frame write_to_framebuffer calls (:619) race at the end."""
+    the cell's corner, raytraced_renderer.cpp:300-318, 622-646) with the binding in place.
+    hook: the binding is told the cell (set_cell, the maintainer's line in render_to_file's cell
+    branch) and renders it as one rectangle — also a cell holding 32-aligned pixels ((32, 16),
+    (32, 32)), which the pixels alone would take for 32x32 tile corners. No hook (ref_driver -C):
+    every pixel of a cell without 32-aligned pixels is queued alone, the lone pixels of a batch
+    merge into rectangles, every batch refreshes the queued pixels' bounding box.
+    The PNG (the cell alone) must equal the product CLI's -p render of the same cell and samples;
+    the rate image the reference binary's own (the sampled pixels are exactly the cell's). One
+    worker: with several, the reference's own unsynchronised whole-frame write_to_framebuffer calls
+    (:619) race at the end."""
     from test_output_stage import CLI, read_png
     W, H, S, M = 64, 48, 64, 5
-    x0, y0, dx, dy = 8, 4, 48, 24
+    x0, y0, dx, dy = cell
     png = str(tmp_path / "cell.png")
-    r = subprocess.run([AMD, "-A", "-t", str(threads), "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-p", str(x0),
+    r = subprocess.run([AMD, "-A"] + ([] if hook else ["-C"]) + ["-t", str(threads), "-s", str(S), "-m", str(M),
+                        "-r", str(W), str(H), "-p", str(x0),
                         str(y0), str(dx), str(dy), "-f", png, os.path.join(REPO, "scenes", "CBgems.dae")],
                        capture_output=True, text=True, timeout=300, cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -18,7 +18,9 @@ CFGS = [("CBspheres_lambertian", 64, 48, 2, 5), ("CBspheres", 64, 48, 2, 5), ("C
         ("CBempty", 64, 48, 2, 5)]
 # the -p cell render (render_to_file's cell branch, raytraced_renderer.cpp:622-646): its PNG is the
 # cell alone, its _rate.png the whole frame; 64 spp so the cell image can be compared statistically
-CELLS = [("CBgems", 64, 48, 64, 5, (8, 4, 48, 24))]
+CELLS = [("CBgems", 64, 48, 64, 5, (8, 4, 48, 24)),
+         # a cell holding 32-aligned pixels ((32, 16), (32, 32)): the binding's set_cell case
+         ("CBgems", 64, 48, 64, 5, (16, 12, 40, 28))]
 
 
 def main():
