@@ -295,7 +295,7 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-depth", type=int, default=None)
-    ap.add_argument("--pipeline", type=int, default=0, help="0 auto, 1 megakernel, 2 wavefront")
+    ap.add_argument("--pipeline", type=int, choices=[0, 1], default=0, help="0 auto = 1 megakernel")
     ap.add_argument("--envmap", default=None,
                     help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
                          "synthetic sky of tools/envmap.py (the reference's exr/*.exr are LFS pointers)")
@@ -461,7 +461,7 @@ def main() -> int:
                    + ("" if dist is None else " + RCCL all-reduce" if args.dist_backend == "nccl"
                       else " + gloo all-reduce"),
                    "workload_key": args.workload if named else "custom",
-                   "pipeline": ["auto (megakernel)", "megakernel", "wavefront"][args.pipeline],
+                   "pipeline": ["auto (megakernel)", "megakernel"][args.pipeline],
                    "scene": os.path.relpath(scene_path, REPO), "width": W, "height": H, "spp": SPP,
                    "max_depth": M, "envmap": env_desc, "russian_roulette": rr,
                    "parallelism": f"{'row bands' if use_pt else 'sample ranges'} x{world}",

@@ -83,7 +83,8 @@ class Tile(C.Structure):
     _fields_ = [("x0", C.c_int32), ("y0", C.c_int32), ("w", C.c_int32), ("h", C.c_int32)]
 
 
-PIPELINE_AUTO, PIPELINE_MEGAKERNEL, PIPELINE_WAVEFRONT = 0, 1, 2
+PIPELINE_AUTO, PIPELINE_MEGAKERNEL = 0, 1
+PIPELINE_WAVEFRONT = 2   # retired in round 5: bdpt_create rejects it
 
 
 class Stats(C.Structure):

@@ -27,6 +27,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BDPT_HD __host__ __device__ __forceinline__
@@ -1319,12 +1321,17 @@ BDPT_HD Vtx vtx_load(const VtxS& s) {
   return v;
 }
 
+// Per-subpath bit masks indexed by the reference's vertex index k <= MAXV + 1: 32 bits up to the
+// m = 16 kernels (unchanged code), 64 for the m <= 32 one.
+template <int MAXV>
+using DeltaMask = typename std::conditional<(MAXV > 29), uint64_t, uint32_t>::type;
+
 template <int MAXV>
 struct Paths {
   VtxS E[MAXV];       // E[k] at index k-2 (k >= 2): eye hits
   VtxS L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
-  uint32_t dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
+  DeltaMask<MAXV> dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
   float l1_dir_pdf;
   f3 l1_d;           // the light walk's first direction and its pdf (read back when it starts)
   float l1_pdf;
@@ -1562,7 +1569,7 @@ BDPT_HD float mis_weight(const SceneView& S, const PA& P, const Vtx* ev, const V
 template <int MAXV, bool EXT>
 struct PathsInRegs {
   const Paths<MAXV>& P;
-  uint32_t dE, dL;
+  DeltaMask<MAXV> dE, dL;
   BDPT_HD explicit PathsInRegs(const Paths<MAXV>& p) : P(p), dE(p.dE), dL(p.dL) {}
   BDPT_HD Vtx e(int k) const { return vtx_load<EXT>(P.E[k - 2]); }
   BDPT_HD Vtx l(int k) const { return vtx_load<EXT>(P.L[k - 1]); }
@@ -1573,12 +1580,14 @@ struct PathsInRegs {
 BDPT_HD f3 walk_next_alpha(f3 pa, f3 pn, f3 d, f3 f, float pdf) { return divs(mul(muls(pa, fabsf(dot(pn, d))), f), pdf); }
 
 // The state of one lane's fused eye + light walk between two iterations (walk_step).
+template <int MAXV>
 struct WalkState {
   f3 ro, rd, prev_n, nalpha;   // the next ray, the previous vertex's normal, the next vertex's throughput
   float rmin, rmax;
   float pv_fwd, pv_gp, pv_q;   // the previous vertex's fwd / prefix / roulette probability
   int i, count, pv_mat;        // reference vertex index, vertices stored on this subpath, previous material
-  uint32_t dm, lpos;           // delta mask of this subpath; the light stream's position after L[1]
+  DeltaMask<MAXV> dm;          // delta mask of this subpath
+  uint32_t lpos;               // the light stream's position after L[1]
   bool light, l1env;           // walking the light subpath; its L[1] is an environment vertex
 };
 
@@ -1586,7 +1595,7 @@ struct WalkState {
 // and the light vertex L[1] with the light walk's first ray (sample_light_ray, :105-118).
 template <int MAXV, bool EXT = false>
 BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
-                        WalkState& w, int x, int y, uint32_t sample) {
+                        WalkState<MAXV>& w, int x, int y, uint32_t sample) {
   rng_init(g, sp.seed, (uint32_t)(x + y * sp.W), sample);
   float px, py;
   grid2d(g, &px, &py);
@@ -1706,11 +1715,11 @@ BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>&
 // subpaths and P.nE / P.nL / P.dE / P.dL complete).
 template <int MAXV, int LM = 0, bool EXT = false>
 BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
-                       WalkState& w) {
+                       WalkState<MAXV>& w) {
   f3 ro = w.ro, rd = w.rd, prev_n = w.prev_n, nalpha = w.nalpha;
   float rmin = w.rmin, rmax = w.rmax, pv_fwd = w.pv_fwd, pv_gp = w.pv_gp, pv_q = w.pv_q;
   int i = w.i, count = w.count, pv_mat = w.pv_mat;
-  uint32_t dm = w.dm;
+  DeltaMask<MAXV> dm = w.dm;
   bool light = w.light, l1env = w.l1env;
   auto next_alpha = walk_next_alpha;
   bool done = false;
@@ -1758,7 +1767,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       v.mat = mat;
       v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
       VtxS* slot = (light ? P.L + 1 : P.E) + count++;
-      if (is_delta(M.type)) dm |= 1u << i;
+      if (is_delta(M.type)) dm |= DeltaMask<MAXV>(1) << i;
       // eye_constants / light_constants of this vertex at its creation. The previous vertex is the
       // one just below it on the same subpath (camera: no step; the light vertex L[1] for the
       // light's first hit) and is still in registers: position ro, normal prev_n (shading axis
@@ -1885,7 +1894,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
 template <int MAXV, int LM = 0, bool EXT = false>
 BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MAXV>& P, Counters& cnt, Rng& g,
                             int x, int y, uint32_t sample) {
-  WalkState w;
+  WalkState<MAXV> w;
   walk_begin<MAXV, EXT>(S, sp, P, cnt, g, w, x, y, sample);
   while (!walk_step<MAXV, LM, EXT>(S, sp, P, cnt, g, w)) {
   }

@@ -1,5 +1,5 @@
-// bdpt_ctx.h — the device context behind the C-ABI handle (shared by the megakernel TU,
-// bdpt_hip.hip, and the wavefront pipeline, bdpt_wavefront.hip).
+// bdpt_ctx.h — the device context behind the C-ABI handle (shared by the kernels' TU,
+// bdpt_hip.hip, and the multi-GPU frame reduce, bdpt_reduce.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,16 +16,11 @@ namespace bdpt {
 
 // bdpt_last_error() text: bdpt_err.h
 
-struct WfState;   // wavefront buffers (bdpt_wavefront.hip)
-
-enum { PIPE_WAVEFRONT = 0, PIPE_MEGAKERNEL = 1 };
-
 struct Ctx {
   HostScene hs;
   bool ext = false;            // environment light or Russian roulette: the EXT kernels
   bdpt_params prm;
   int device = 0;
-  int pipeline = PIPE_WAVEFRONT;
   hipStream_t own = nullptr, stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -64,13 +59,12 @@ struct Ctx {
   // worker threads (raytraced_renderer.cpp:325-327,610-615); calls on one ctx are serialised here.
   std::recursive_mutex mu;
   // Diagnostics read once at bdpt_create (BDPT_LDS_MODE, BDPT_NTOP_MAX, BDPT_BLOCK_MAJOR,
-  // BDPT_XCD_GROUPS, BDPT_PIPELINE): -1 = not set.
+  // BDPT_XCD_GROUPS): -1 = not set.
   int env_lds_mode = -1, env_ntop_max = -1, block_major = 1, xcd = 0;
   int last_lm = -1;            // LDS mode of the last BDPT / PathTracer launch
   int maxv = 5;
   int ncu = 256;
   size_t npix = 0;
-  WfState* wf = nullptr;
 };
 
 #define HIPCHK(x)                                                                   \
@@ -119,10 +113,5 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.env.rad = hs.env_rad;
   return S;
 }
-
-// Wavefront pipeline (bdpt_wavefront.hip). blocks: device list of 8x8 pixel blocks (x0, y0, w, h)
-// or null for the full frame (nbx blocks per row).
-int wf_render(Ctx* c, const int4* blocks, int nblocks, int nbx, int spp_begin, int spp_count);
-void wf_free(Ctx* c);
 
 }  // namespace bdpt

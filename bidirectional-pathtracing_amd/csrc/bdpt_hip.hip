@@ -63,6 +63,8 @@ __device__ __forceinline__ int wave_max(int v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
   return v;
 }
+__device__ __forceinline__ int ctz_mask(uint32_t m) { return __builtin_ctz(m); }
+__device__ __forceinline__ int ctz_mask(uint64_t m) { return __builtin_ctzll(m); }
 // number of set bits of m below this lane (ballot + mbcnt prefix sum)
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -163,6 +165,7 @@ constexpr int kLdsMats = 48, kLdsLights = 8;
 constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 1 (when it fits) and 2
 
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
+constexpr int kMaxDepth = 32;   // the deepest k_bdpt_sample instantiation (MAXV = 32)
 
 #ifdef BDPT_PHASE_PROF
 #define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
@@ -347,14 +350,15 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
   // ... then the general (i >= 2, j >= 2) pairs from per-lane lists of connectable vertices:
   // a lane walks its own (i, j) pairs, so the wave iterates max(pairs) times instead of
   // max|E| x max|L| (most cells of that grid are empty for most lanes)
-  unsigned mE = 0, mL = 0;
-  for (int k = 2; k < nE; k++) mE |= (PP.e(k).cq > 0.0f ? 1u : 0u) << k;
-  for (int k = 2; k < nL; k++) mL |= (PP.l(k).cq > 0.0f ? 1u : 0u) << k;
+  using Mask = decltype(PP.dE);   // 32 bits, or 64 for the m <= 32 kernel
+  Mask mE = 0, mL = 0;
+  for (int k = 2; k < nE; k++) mE |= Mask(PP.e(k).cq > 0.0f ? 1u : 0u) << k;
+  for (int k = 2; k < nL; k++) mL |= Mask(PP.l(k).cq > 0.0f ? 1u : 0u) << k;
   if (mL == 0) mE = 0;
-  unsigned jm = mL;
+  Mask jm = mL;
   while (__ballot(mE != 0)) {
     const bool act = mE != 0;
-    const int ci = act ? __builtin_ctz(mE) : 0, cj = act ? __builtin_ctz(jm) : 0;
+    const int ci = act ? ctz_mask(mE) : 0, cj = act ? ctz_mask(jm) : 0;
     conn_step(ci, cj, act);
     if (act) {
       jm &= jm - 1;
@@ -696,7 +700,6 @@ void free_ctx(Ctx* c) {
                   c->d_eye, c->d_light, c->d_sample, c->d_stats};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
-  wf_free(c);
   for (Ctx::BlockSlot& b : c->blk) {
     if (b.d) (void)hipFree(b.d);
     if (b.h) (void)hipHostFree(b.h);
@@ -731,15 +734,30 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
     g_err = "invalid frame size / spp / max_depth";
     return BDPT_E_INVALID;
   }
+  // the kernels hold a subpath in a fixed array: instantiations for m <= 5, 8, 16 and 32 (the
+  // reference's vectors have no cap, bidirection.cpp:84-86; deeper paths are rejected cleanly)
   int need = p.max_depth < 1 ? 1 : p.max_depth;
-  if (need > 16) { g_err = "max_depth > 16 not compiled"; return BDPT_E_UNSUPPORTED; }
+  if (need > kMaxDepth) {
+    g_err = "max_depth " + std::to_string(p.max_depth) + " > " + std::to_string(kMaxDepth) +
+            ": the deepest kernel holds subpaths of up to 32 bounces";
+    return BDPT_E_UNSUPPORTED;
+  }
+  // 0 = auto = 1: the persistent megakernel. 2 was the wavefront pipeline (per-bounce kernels with
+  // ballot-compacted ray queues), retired in round 5 after it had fallen to 0.32-0.50x of the
+  // megakernel and never ran the environment light / roulette.
+  if (p.integrator == BDPT_INTEGRATOR_PT && p.max_depth > kPtMaxVerts) {   // k_pt records <= 21 vertices
+    g_err = "PathTracer max_depth " + std::to_string(p.max_depth) + " > " + std::to_string(kPtMaxVerts) +
+            ": its walk records up to 21 vertices (the reference's own roulette cap, pathtracer.cpp:215)";
+    return BDPT_E_UNSUPPORTED;
+  }
+  if (p.pipeline == 2) {
+    g_err = "pipeline 2 (wavefront) was retired: it ran at 0.32-0.50x of the megakernel (DESIGN.md §5); use 0 or 1";
+    return BDPT_E_UNSUPPORTED;
+  }
+  if (p.pipeline < 0 || p.pipeline > 2) { g_err = "bad pipeline (0 = auto, 1 = megakernel)"; return BDPT_E_INVALID; }
   Ctx* c = new Ctx();
   c->prm = p;
-  c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : 16;
-  // 0 = auto: the megakernel (measured faster on the reference's Cornell-box scenes), 1 =
-  // megakernel, 2 = wavefront. BDPT_PIPELINE overrides (diagnostics / A-B runs).
-  int pipe = p.pipeline;
-  if (const char* pe = getenv("BDPT_PIPELINE")) pipe = atoi(pe);
+  c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : need <= 16 ? 16 : 32;
   // diagnostics / A-B switches, read once per ctx (tests set them before bdpt_create)
   auto env_int = [](const char* name, int dflt) { const char* v = getenv(name); return v ? atoi(v) : dflt; };
   c->env_lds_mode = env_int("BDPT_LDS_MODE", -1);
@@ -747,7 +765,6 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->block_major = env_int("BDPT_BLOCK_MAJOR", 1);
   c->xcd = env_int("BDPT_XCD_GROUPS", 0);
   if (c->env_lds_mode > 3) { g_err = "BDPT_LDS_MODE must be 0..3"; delete c; return BDPT_E_INVALID; }
-  c->pipeline = pipe == 2 ? PIPE_WAVEFRONT : PIPE_MEGAKERNEL;
   c->pt = p.integrator == BDPT_INTEGRATOR_PT;
   if (p.integrator != BDPT_INTEGRATOR_BDPT && !c->pt) { g_err = "unknown integrator"; delete c; return BDPT_E_INVALID; }
   if (c->pt && (p.ns_area_light < 0 || p.samples_per_batch < 0 || p.lens_radius < 0)) {
@@ -756,11 +773,6 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   int rc = build_host_scene(scene, c->hs, g_err, c->pt);
   if (rc) { delete c; return rc; }
   c->ext = c->hs.env_light >= 0 || p.russian_roulette != 0;
-  if (c->ext && !c->pt && c->pipeline == PIPE_WAVEFRONT) {
-    g_err = "the wavefront pipeline does not implement the environment light / Russian roulette; use pipeline 0 or 1";
-    delete c;
-    return BDPT_E_UNSUPPORTED;
-  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
     g_err = "no HIP device";
@@ -932,14 +944,6 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
     c->timed = true;
     return BDPT_OK;
   }
-  if (c->pipeline == PIPE_WAVEFRONT) {
-    HIPCHK(hipEventRecord(c->ev0, c->stream));
-    int rc = wf_render(c, kp.blocks, kp.nblocks, kp.nbx, spp_begin, spp_count);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(c->ev1, c->stream));
-    c->timed = true;
-    return BDPT_OK;
-  }
   int spl = c->prm.samples_per_lane;
   if (spl <= 0) {
     // small work items (8x8 pixels x 2 samples): measured against the earlier "~16 items per
@@ -966,7 +970,8 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.xcd = c->xcd;
   if (kp.xcd) HIPCHK(hipMemsetAsync(kp.work8, 0, 8 * 32 * sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp) : launch_maxv<16>(c, kp);
+  int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp)
+           : c->maxv == 16 ? launch_maxv<16>(c, kp) : launch_maxv<32>(c, kp);
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->timed = true;

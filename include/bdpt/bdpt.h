@@ -146,7 +146,8 @@ typedef struct bdpt_params {
   int32_t samples_per_lane;   /* 0 = auto                                                 */
   int32_t device;             /* HIP device ordinal                                       */
   int32_t collect_stats;      /* 1 = kernel also counts node/prim tests (roofline bytes)  */
-  int32_t pipeline;           /* 0 = auto, 1 = megakernel, 2 = wavefront; same results     */
+  int32_t pipeline;           /* 0 = auto = 1, the megakernel; 2 (the wavefront pipeline) was
+                                 retired in round 5: BDPT_E_UNSUPPORTED                      */
   int32_t russian_roulette;   /* 1 = PathVertex.q roulette on both subpaths (ABI v2)       */
   /* ABI v3: the integrator and the PathTracer's settings (PathTracer fields, pathtracer.h:73-85;
    * CLI -l -a -H -b -d, main.cpp:107-141; AppConfig defaults application.h:45-65) */

@@ -166,8 +166,8 @@ def test_russian_roulette_unbiased():
     assert np.abs(mb / ma - 1).max() < 0.02, (ma, mb)
 
 
-def test_env_requires_megakernel():
-    """The wavefront pipeline does not implement the extensions: rejected before any device call."""
+def test_retired_wavefront_pipeline_rejected():
+    """pipeline 2 (the wavefront pipeline, retired in round 5) is rejected before any device call."""
     sc = _scene_with("sky_32x16_zip_half")
     p = B.Params()
     p.width, p.height, p.spp, p.max_depth = 32, 24, 1, 5

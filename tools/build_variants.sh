@@ -8,7 +8,7 @@
 cd "$(dirname "$0")/.." || exit 1
 CS=bidirectional-pathtracing_amd/csrc
 FL="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -fPIC -Iinclude -I$CS"
-UNITS="bdpt_hip.hip bdpt_wavefront.hip bdpt_scene.cpp dae_loader.cpp exr_loader.cpp"
+UNITS="bdpt_hip.hip bdpt_reduce.hip bdpt_scene.cpp dae_loader.cpp exr_loader.cpp"
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//,/ }
   mkdir -p build/var/$name
