@@ -287,8 +287,35 @@ struct Counters {
   unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
   unsigned long long clk_light = 0;        // ... drawing the light vertex L[1] (sample_light_ray)
   unsigned long long clk_vertex = 0;       // ... from a hit to the next ray (shading record, vertex, sample_f)
+  // lane use per phase: [2k] wave-level iterations (counted by the wave's lowest active lane),
+  // [2k + 1] active lanes summed over them (every active lane counts itself); k = LP_*
+  uint32_t lp[2 * 8] = {};
 #endif
 };
+
+// Phases of the lane-use profile (BDPT_PHASE_PROF builds, bdpt_debug_lane_counters).
+enum {
+  LP_CNODE = 0,   // closest-hit node steps (walk rays)
+  LP_CPRIM = 1,   // closest-hit primitive tests
+  LP_ANODE = 2,   // any-hit node steps (connection rays)
+  LP_APRIM = 3,   // any-hit primitive tests
+  LP_SHADE = 4,   // walk: hit -> next ray (shading record, vertex, MIS constants, sample_f)
+  LP_WALK = 5,    // walk iterations (one closest-hit query each)
+  LP_CONN = 6,    // connection evaluations (make_conn)
+  LP_FLUSH = 7    // connection-ray flushes: wave-level flushes / rays traced
+};
+#if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define BDPT_LANE_PROF(c, k)                                                                      \
+  do {                                                                                            \
+    const unsigned long long m_ = __ballot(1);                                                    \
+    if ((unsigned)__lane_id() == (unsigned)__builtin_ctzll(m_)) (c).lp[2 * (k)]++;                \
+    (c).lp[2 * (k) + 1]++;                                                                        \
+  } while (0)
+#else
+#define BDPT_LANE_PROF(c, k) \
+  do {                       \
+  } while (0)
+#endif
 
 struct Hit {
   float t;
@@ -709,6 +736,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     // the flat list as one run of primitives, the next record's loads issued before this test
     float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
     for (int pi = 0; pi < S.fn; pi++) {
+      BDPT_LANE_PROF(c, LP_CPRIM);
       const float4 g0 = a0, g1 = a1, g2 = a2;
       const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
       a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
@@ -739,6 +767,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
+      BDPT_LANE_PROF(c, LP_CPRIM);
       const int pi = st + k;
       float t, b1 = 0, b2 = 0;
       bool ok;
@@ -782,6 +811,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     int pend = 0;
     for (;;) {
       while (ref >= 0) {
+        BDPT_LANE_PROF(c, LP_CNODE);
         ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
@@ -805,7 +835,10 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         if (li >= S.nleaves) break;
         ref = ld_lds_i(S.lleaves + li++);
       }
-      while (ref >= 0) ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
+      while (ref >= 0) {
+        BDPT_LANE_PROF(c, LP_CNODE);
+        ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
+      }
       if (ref == kTravDone) break;
       test_leaf(ref);
       if (LM != 3 && !stk.pop(ref)) break;
@@ -827,6 +860,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   if (LM == 3 && S.fn > 0) {
     float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
     for (int pi = 0; pi < S.fn; pi++) {
+      BDPT_LANE_PROF(c, LP_APRIM);
       const float4 g0 = a0, g1 = a1, g2 = a2;
       const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
       a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
@@ -851,6 +885,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
     }
     for (int k = 0; k < cnt; k++) {
+      BDPT_LANE_PROF(c, LP_APRIM);
       const int pi = st + k;
       float t, b1, b2;
       bool ok;
@@ -883,6 +918,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
     int pend = 0;
     for (;;) {
       while (ref >= 0) {
+        BDPT_LANE_PROF(c, LP_ANODE);
         ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
@@ -906,7 +942,10 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
         if (li >= S.nleaves) return false;
         ref = ld_lds_i(S.lleaves + li++);
       }
-      while (ref >= 0) ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
+      while (ref >= 0) {
+        BDPT_LANE_PROF(c, LP_ANODE);
+        ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
+      }
       if (ref == kTravDone) return false;
       if (test_leaf(ref)) return true;
       if (LM != 3 && !stk.pop(ref)) return false;
@@ -1728,6 +1767,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
 #endif
+    BDPT_LANE_PROF(cnt, LP_WALK);
     bool end = !trace_closest<LM, kWalkStack>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
@@ -1753,6 +1793,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       vtx_store<EXT>(P.E[count++], v);
     }
     if (!end) {
+      BDPT_LANE_PROF(cnt, LP_SHADE);
       f3 n;
       int mat;
       shade_hit<LM>(S, h, ro, rd, &n, &mat);

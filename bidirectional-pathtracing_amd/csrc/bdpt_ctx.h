@@ -39,8 +39,9 @@ struct Ctx {
   float* d_eye = nullptr;
   float* d_light = nullptr;
   float* d_sample = nullptr;
-  // [0..7] counters, [12..14] environment-table reads, [15] tickets, [16..31] phase profile
-  static constexpr int kStatSlots = 32;
+  // [0..7] counters, [12..14] environment-table reads, [15] tickets, [16..31] phase profile,
+  // [32..47] lane-use profile (BDPT_PHASE_PROF builds)
+  static constexpr int kStatSlots = 48;
   unsigned long long* d_stats = nullptr;
   // Tile-block lists of bdpt_render: a ring of pinned staging + device buffers, each slot reused
   // only after the event recorded behind the launch that read it, so back-to-back tile renders

@@ -96,6 +96,10 @@ __device__ __forceinline__ void flush_queue(const SceneView& S, WaveQ& q, int he
   bool vis = false;
   float vx = 0, vy = 0, vz = 0;
   int tgt = -1;
+#ifdef BDPT_PHASE_PROF
+  if (lane == 0) cnt.lp[2 * LP_FLUSH]++;
+  if (lane < n) cnt.lp[2 * LP_FLUSH + 1]++;
+#endif
   if (lane < n) {
     const int k = (head + lane) & (QCAP - 1);
     f3 o = mk3(q.ox[k], q.oy[k], q.oz[k]), d = mk3(q.dx[k], q.dy[k], q.dz[k]);
@@ -166,6 +170,8 @@ constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   //
 
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
 constexpr int kMaxDepth = 32;   // the deepest k_bdpt_sample instantiation (MAXV = 32)
+#define BDPT_STR2(x) #x
+#define BDPT_STR(x) BDPT_STR2(x)
 
 #ifdef BDPT_PHASE_PROF
 #define PH_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
@@ -305,6 +311,7 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
     int kind = CONN_NONE;
     Conn cn;
     if (active) {
+      BDPT_LANE_PROF(cnt, LP_CONN);
       kind = make_conn<EXT>(kp.S, kp.sp, PP, g, i, j, cn, ev_pre, lv_pre, EXT && STATS ? &cnt : nullptr);
       if (kind == CONN_DIRECT) {
         // straight into this lane's accumulator in the wave's LDS (only this wave writes it, and
@@ -481,6 +488,11 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
     atomicAdd((unsigned long long*)kp.prof + 6, ph_cells);
     atomicAdd((unsigned long long*)kp.prof + 8, cnt.clk_light);
     atomicAdd((unsigned long long*)kp.prof + 9, cnt.clk_vertex);
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {   // lane-use profile: prof[16 + k]
+    const unsigned long long s = (unsigned long long)wave_sum(cnt.lp[k]);
+    if (lane == 0 && s) atomicAdd((unsigned long long*)kp.prof + 16 + k, s);
   }
   {
     const unsigned long long wl = (unsigned long long)wave_sum((unsigned)ph_walk_lane);
@@ -970,8 +982,13 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.xcd = c->xcd;
   if (kp.xcd) HIPCHK(hipMemsetAsync(kp.work8, 0, 8 * 32 * sizeof(unsigned), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
+#ifdef BDPT_ONLY_MAXV   // A/B variant builds (tools/build_variants.sh): one depth class, a faster compile
+  if (c->maxv != BDPT_ONLY_MAXV) { g_err = "variant build: only max_depth class " BDPT_STR(BDPT_ONLY_MAXV); return BDPT_E_UNSUPPORTED; }
+  int rc = launch_maxv<BDPT_ONLY_MAXV>(c, kp);
+#else
   int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp)
            : c->maxv == 16 ? launch_maxv<16>(c, kp) : launch_maxv<32>(c, kp);
+#endif
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->timed = true;
@@ -1087,6 +1104,16 @@ int bdpt_get_stats(void* ctx, bdpt_stats* out) {
   out->env_samples = s[12];
   out->env_lookups = s[13];
   out->env_pdf_lookups = s[14];
+  return BDPT_OK;
+}
+
+int bdpt_debug_lane_counters(void* ctx, uint64_t* out16) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !out16) { g_err = "null argument"; return BDPT_E_INVALID; }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out16, c->d_stats + 32, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return BDPT_OK;
 }
 

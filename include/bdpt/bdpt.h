@@ -270,6 +270,11 @@ int bdpt_trace_rays(void* ctx, const float* rays, int32_t n, int32_t any_hit, fl
  * connection generation and connection rays, walk traversal; walk iterations per wave / per lane;
  * connection-grid cells / pairs). Sync. */
 int bdpt_debug_counters(void* ctx, uint64_t* out16);
+/* Diagnostic hook (ABI v9): the lane-use profile of a BDPT_PHASE_PROF build — per phase k (closest-hit
+ * node steps, closest-hit primitive tests, any-hit node steps, any-hit primitive tests, walk
+ * shading, walk iterations, connection evaluations, connection-ray flushes) out16[2k] = wave-level
+ * iterations and out16[2k+1] = active lanes summed over them. Sync. Zero in product builds. */
+int bdpt_debug_lane_counters(void* ctx, uint64_t* out16);
 
 /* Host-side COLLADA loader: the reference CLI's scene path (ColladaParser::load,
  * collada.cpp:129-941, + Application::load, application.cpp:228-304). width/height > 0 apply

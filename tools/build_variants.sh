@@ -1,5 +1,6 @@
 #!/bin/bash
 # Builds A/B variants of libbdpt_amd.so: VARIANTS="name:FLAGS name2:FLAGS2 ..." -> build_var_<name>.so
+# (a flag -DBDPT_ONLY_MAXV=5 compiles one depth class only: m <= 5, a quarter of the compile time)
 # Every translation unit of a variant is compiled with that variant's flags into its own
 # directory (build/var/<name>/): a variant never links objects built with other macro settings or
 # against an older bdpt_ctx.h (round 1's phase-profile run linked a stale bdpt_wavefront.hip.o whose
@@ -21,6 +22,6 @@ for v in $VARIANTS; do
   name=${v%%:*}
   objs=""
   for u in $UNITS; do objs="$objs build/var/$name/$u.o"; done
-  hipcc $FL -shared -o build_var_$name.so $objs -lz || exit 1
+  hipcc $FL -shared -o build_var_$name.so $objs -lz -ldl || exit 1
 done
 ls -la build_var_*.so

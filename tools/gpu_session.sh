@@ -1,0 +1,61 @@
+#!/bin/bash
+# The GPU session script (round 5 onward; earlier per-round scripts are in tools/archive/).
+#   PART=tests    the whole `pytest -m gpu` suite
+#   PART=phases   phase split + lane use per phase (BDPT_PHASE_PROF variants build_var_ph.so (m <= 5)
+#                 and build_var_ph8.so (m <= 8), tools/build_variants.sh) on the north star and C5
+#   PART=bench    bench.py on WORKLOADS (default: ns c2 c3 c4 c5); ROCPROF=1 adds the rocprofv3
+#                 kernel stats of the default line
+#   PART=ab       A/B of variant libraries: LIBS="build_var_a.so build_var_b.so ..." on CFGS
+#                 (prof_render.py argument strings separated by ';'), ROUNDS interleaved rounds
+#   PART=full     tests, then bench
+# Every GPU step runs under its own timeout; the script stops at the first abort / fault / timeout.
+cd "$(dirname "$0")/.." || exit 1
+OUT=gpurun_out/${TAG:-r05}
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name, timeout, cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n ${TAIL:-3} "$OUT/$name.log" | cut -c1-3000
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+PART=${PART:-tests}
+if [ "$PART" = tests ] || [ "$PART" = full ]; then
+  step pytest_gpu 1000 $PYT tests -m gpu
+fi
+if [ "$PART" = phases ]; then
+  TAIL=30
+  step ph_ns 300 env BDPT_LIB=$PWD/build_var_ph.so BDPT_PHASES=1 python3 tools/prof_render.py scenes/CBlucy_standin.dae 1920 1080 8 5 1
+  step ph_c5 300 env BDPT_LIB=$PWD/build_var_ph8.so BDPT_PHASES=1 BDPT_ENV=synth:1024x512 BDPT_RR=1 python3 tools/prof_render.py scenes/CBlucy_standin.dae 1920 1080 8 8 1
+  step ph_c2 300 env BDPT_LIB=$PWD/build_var_ph.so BDPT_PHASES=1 python3 tools/prof_render.py CBspheres 480 360 32 5 1
+  step ph_c4 300 env BDPT_LIB=$PWD/build_var_ph8.so BDPT_PHASES=1 python3 tools/prof_render.py scenes/CBgems.dae 1920 1080 8 7 1
+fi
+if [ "$PART" = ab ]; then
+  IFS=';' read -ra cfgs <<< "${CFGS:-scenes/CBlucy_standin.dae 1920 1080 32 5 2}"
+  for r in $(seq 1 ${ROUNDS:-2}); do
+    for c in "${cfgs[@]}"; do
+      for lib in $LIBS; do
+        # "c5 ARGS": the C5 shape (synthetic sky + roulette) on ARGS
+        envx=""; a="$c"
+        case "$c" in c5\ *) envx="BDPT_ENV=synth:1024x512 BDPT_RR=1"; a=${c#c5 } ;; esac
+        step ab_r${r}_$(basename $lib .so)_$(echo $c | tr ' /.' '___') 300 env BDPT_LIB=$PWD/$lib $envx python3 tools/prof_render.py $a
+      done
+    done
+  done
+fi
+if [ "$PART" = bench ] || [ "$PART" = full ]; then
+  for w in ${WORKLOADS:-ns c2 c3 c4 c5}; do
+    extra=""; [ "$w" != ns ] && extra="--no-cpu-baseline"
+    [ "$w" = c4 ] || [ "$w" = c5 ] && extra="$extra --steps 2"
+    step bench_$w 900 python bench.py --workload $w $extra
+  done
+  if [ -n "$ROCPROF" ]; then
+    step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
+  fi
+fi
+echo "== done"

@@ -54,6 +54,18 @@ if os.environ.get("BDPT_PHASES"):
           "connection cells %.4g x 64, (i, j) pairs %.4g -> %.1f%%" % (
               arr[4], arr[5], 100 * arr[5] / max(1, 64 * arr[4]), arr[6], arr[7],
               100 * arr[7] / max(1, 64 * arr[6])))
+    lane = (C.c_uint64 * 16)()
+    pt.lib.bdpt_debug_lane_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    pt.lib.bdpt_debug_lane_counters(pt.ctx, lane)
+    names = ["closest-hit node steps", "closest-hit prim tests", "any-hit node steps", "any-hit prim tests",
+             "walk shading (hit -> next ray)", "walk iterations", "connection evaluations (make_conn)",
+             "connection-ray flushes (rays)"]
+    print("  lane use per phase: wave-level iterations, mean active lanes of 64, share of all wave-iterations")
+    tw = sum(lane[2 * k] for k in range(8) if k != 5)
+    for k, nm in enumerate(names):
+        w_, l_ = lane[2 * k], lane[2 * k + 1]
+        print(f"    {nm:38s} {w_:14d}  {l_ / max(1, w_):6.2f} / 64 = {100 * l_ / max(1, 64 * w_):5.1f}%"
+              + ("" if k == 5 else f"   {100 * w_ / max(1, tw):5.1f}% of iterations"))
 if os.environ.get("BDPT_STATS") == "1":
     st = pt.stats()
     n = max(1, st.samples)
