@@ -40,9 +40,14 @@ if [ "$PART" = ab ]; then
   for r in $(seq 1 ${ROUNDS:-2}); do
     for c in "${cfgs[@]}"; do
       for lib in $LIBS; do
-        # "c5 ARGS": the C5 shape (synthetic sky + roulette) on ARGS
-        envx=""; a="$c"
-        case "$c" in c5\ *) envx="BDPT_ENV=synth:1024x512 BDPT_RR=1"; a=${c#c5 } ;; esac
+        # leading KEY=VAL words are environment (e.g. BDPT_LDS_MODE=0); "c5" = the C5 shape
+        # (synthetic sky + roulette)
+        envx=""; a=""
+        for wd in $c; do
+          if [ -z "$a" ] && [[ "$wd" == *=* ]]; then envx="$envx $wd"
+          elif [ -z "$a" ] && [ "$wd" = c5 ]; then envx="$envx BDPT_ENV=synth:1024x512 BDPT_RR=1"
+          else a="$a $wd"; fi
+        done
         step ab_r${r}_$(basename $lib .so)_$(echo $c | tr ' /.' '___') 300 env BDPT_LIB=$PWD/$lib $envx python3 tools/prof_render.py $a
       done
     done
