@@ -273,8 +273,6 @@ struct SceneView {
   int ntop;
   int* lstack;           // LM 1 / 2: the traversal stacks' first kLdsStack overflow slots in LDS (slot k of
                          // lane t at lstack[k * kLdsStackStride + t]); null: all overflow in scratch
-  float4* lleaf;         // BDPT_GLDS_LEAF experiment: per-lane LDS slots of a postponed leaf's first
-                         // primitive record (3 x 64 float4 per wave), filled by LDS-DMA; null: off
   DCam cam;
   EnvView env;
 };
@@ -458,36 +456,6 @@ BDPT_HD constexpr int node_bytes(int W) { return 16 * node_f4(W); }
 // 471 / 465, CBbunny 800x600 510 / 517 / 515 / 508.
 constexpr int kLdsStack = 8;
 constexpr int kLdsStackStride = 1024;   // lanes per block (bdpt_hip.hip kBlock)
-
-#ifdef BDPT_GLDS_LEAF
-// Experiment: when a lane's descent postpones a leaf (speculative traversal), the leaf's first
-// primitive record is fetched by LDS-DMA (global_load_lds_dwordx4 x 3, no VGPR destination) into
-// this lane's LDS slots, so that it arrives while the wave finishes its descent and test_leaf reads
-// it from LDS instead of starting a dependent global load.
-BDPT_HD void leaf_rec_prefetch(const SceneView& S, int lf) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  typedef __attribute__((address_space(3))) float4 lf4;
-  lf4* base = (lf4*)S.lleaf + wv * 192;
-  const __attribute__((address_space(1))) char* src =
-      (const __attribute__((address_space(1))) char*)(S.geom + 3 * leaf_start(lf));
-  __builtin_amdgcn_global_load_lds(src, base, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(src + 16, base + 64, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(src + 32, base + 128, 16, 0, 0);
-#endif
-}
-BDPT_HD void leaf_rec_first(const SceneView& S, int lf, float4& a0, float4& a1, float4& a2) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const float4* p = S.lleaf + (threadIdx.x >> 6) * 192 + (threadIdx.x & 63);
-  a0 = *(const __attribute__((address_space(3))) float4*)p;
-  a1 = *(const __attribute__((address_space(3))) float4*)(p + 64);
-  a2 = *(const __attribute__((address_space(3))) float4*)(p + 128);
-#else
-  const float4* p = S.geom + 3 * leaf_start(lf);
-  a0 = p[0]; a1 = p[1]; a2 = p[2];
-#endif
-}
-#endif
 
 // this lane's LDS overflow slots (device, LM 1 / 2 kernels that staged them), else null
 BDPT_HD int* lane_stack(const SceneView& S) {
@@ -796,11 +764,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   auto test_leaf = [&](int lf) {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM)) {
-#ifdef BDPT_GLDS_LEAF
-      leaf_rec_first(S, lf, a0, a1, a2);
-#else
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
-#endif
     }
     for (int k = 0; k < cnt; k++) {
       BDPT_LANE_PROF(c, LP_CPRIM);
@@ -851,9 +815,6 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
-#ifdef BDPT_GLDS_LEAF
-          leaf_rec_prefetch(S, pend);
-#endif
           if (!stk.pop(ref)) ref = kTravDone;
         }
         if (wave_count(pend == 0 && ref >= 0) == 0) break;
@@ -863,9 +824,6 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         pend = 0;
         if (ref < 0 && ref != kTravDone) {
           pend = ref;
-#ifdef BDPT_GLDS_LEAF
-          leaf_rec_prefetch(S, pend);
-#endif
           if (!stk.pop(ref)) ref = kTravDone;
         }
       }
@@ -924,11 +882,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   auto test_leaf = [&](int lf) -> bool {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM)) {
-#ifdef BDPT_GLDS_LEAF
-      leaf_rec_first(S, lf, a0, a1, a2);
-#else
       a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
-#endif
     }
     for (int k = 0; k < cnt; k++) {
       BDPT_LANE_PROF(c, LP_APRIM);
@@ -968,9 +922,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
         ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
         if (ref < 0 && ref != kTravDone && pend == 0) {
           pend = ref;
-#ifdef BDPT_GLDS_LEAF
-          leaf_rec_prefetch(S, pend);
-#endif
           if (!stk.pop(ref)) ref = kTravDone;
         }
         if (wave_count(pend == 0 && ref >= 0) == 0) break;
@@ -980,9 +931,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
         pend = 0;
         if (ref < 0 && ref != kTravDone) {
           pend = ref;
-#ifdef BDPT_GLDS_LEAF
-          leaf_rec_prefetch(S, pend);
-#endif
           if (!stk.pop(ref)) ref = kTravDone;
         }
       }
@@ -1423,9 +1371,6 @@ struct Paths {
   VtxS L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
   DeltaMask<MAXV> dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
-#ifdef BDPT_BOUND_WB2
-  VtxS X[2 * MAXV + 1];   // timing experiment: a second copy of every stored hit vertex (never read)
-#endif
   float l1_dir_pdf;
   f3 l1_d;           // the light walk's first direction and its pdf (read back when it starts)
   float l1_pdf;
@@ -1911,9 +1856,6 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       };
       if (!EXT) finish(1.0f);
       vtx_store<EXT>(*slot, v);
-#ifdef BDPT_BOUND_WB2
-      vtx_store<EXT>(P.X[(light ? MAXV : 0) + count - 1], v);
-#endif
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
         if (EXT) {

@@ -62,7 +62,6 @@ struct Ctx {
   // Diagnostics read once at bdpt_create (BDPT_LDS_MODE, BDPT_NTOP_MAX, BDPT_BLOCK_MAJOR,
   // BDPT_XCD_GROUPS): -1 = not set.
   int env_lds_mode = -1, env_ntop_max = -1, block_major = 1, xcd = 0;
-  int glds = 0;   // BDPT_GLDS (BDPT_GLDS_LEAF builds): 1 = LDS-DMA leaf-record prefetch
   int last_lm = -1;            // LDS mode of the last BDPT / PathTracer launch
   int maxv = 5;
   int ncu = 256;
@@ -97,7 +96,6 @@ inline SceneView view_of(const Ctx* c, int LM) {
   S.fn = flat_prims(c->hs, &S.fsph);
   S.ntop = 0;
   S.lstack = nullptr;
-  S.lleaf = nullptr;
   S.cam = c->hs.cam;
   const HostScene& hs = c->hs;
   S.env.light = hs.env_light;

@@ -51,7 +51,6 @@ struct KParams {
   int nmat;
   unsigned item_lo;           // first item of this launch (tickets count from it)
   int lstack_on;              // the traversal stacks' LDS overflow slots are staged (LM 1 / 2)
-  int leaf_on;                // BDPT_GLDS_LEAF experiment: the leaf-record slots follow the wave queues
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -170,7 +169,6 @@ constexpr int kLdsMats = 48, kLdsLights = 8;
 constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 1 (when it fits) and 2
 
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
-constexpr size_t kLeafBufBytes = (size_t)kWavesPerBlock * 3 * 64 * 16;   // BDPT_GLDS_LEAF: 48 KB
 constexpr int kMaxDepth = 32;   // the deepest k_bdpt_sample instantiation (MAXV = 32)
 #define BDPT_STR2(x) #x
 #define BDPT_STR(x) BDPT_STR2(x)
@@ -190,10 +188,8 @@ __device__ __forceinline__ void stage_scene(KParams& kp, unsigned char* smem, DM
   const bool lst = (LM == 1 || LM == 2) && kLdsStack > 0 && kp.lstack_on;
   if (lst)   // the traversal stacks' LDS overflow slots, behind the wave queues
     kp.S.lstack = (int*)(smem + kWavesPerBlock * sizeof(WaveQ));
-  const size_t leaf_off = kWavesPerBlock * sizeof(WaveQ) + (lst ? kLdsStackBytes : 0);
-  if (kp.leaf_on) kp.S.lleaf = (float4*)(smem + leaf_off);
   if (LM != 0) {
-    float4* sc = (float4*)(smem + leaf_off + (kp.leaf_on ? kLeafBufBytes : 0));
+    float4* sc = (float4*)(smem + kWavesPerBlock * sizeof(WaveQ) + (lst ? kLdsStackBytes : 0));
     const int nn = LM == 1 ? kp.n_node4 : LM == 3 ? 0 : node_f4(lm_width(LM)) * kp.S.ntop;
     const int n4 = nn + (LM == 1 || LM == 3 ? kp.n_geom4 : 0);
     for (int k = threadIdx.x; k < n4; k += blockDim.x)
@@ -475,9 +471,6 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
       ph_pairs += (unsigned)(max(nE - 1, 0) * nL);
 #endif
       connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV, EXT>(P), g, nE, nL, lane, inv, cs, cnt);
-#ifdef BDPT_BOUND_WB2
-      if (__builtin_expect(nE == -12345, 0)) cnt.tris += P.X[t & 7].mb;   // keeps the copies' stores
-#endif
     }
     finish_item<LM>(kp, q, it, lane, cs, cnt);
 #ifdef BDPT_PHASE_PROF
@@ -660,19 +653,7 @@ int pick_lm(Ctx* c, KParams& kp, size_t* lds) {
   // LM 2 always gives the stacks their LDS slots (the treelet makes room); LM 1 when the whole
   // scene and the slots fit together (CBgems: +0.5 .. +0.8 %, profiles/r04o_ab_stack_lm1.log)
   kp.lstack_on = lm == 2 || (lm == 1 && full + kLdsStackBytes <= kLdsSceneMax);
-  kp.leaf_on = 0;
-#ifdef BDPT_GLDS_LEAF
-  // experiment: BDPT_GLDS=1 gives LM 0 the leaf-record slots; =2 also LM 2, whose stack slots and
-  // part of the treelet make room
-  // (the experiment build always reads the slots in LM 0 / 2: they are always given)
-  if (lm == 0) kp.leaf_on = 1;
-  if (lm == 2) {
-    kp.leaf_on = 1;
-    kp.lstack_on = 0;
-    kp.S.ntop = (int)std::min<size_t>((size_t)kp.S.ntop, (kLdsSceneMax - kLeafBufBytes) / node_bytes(lm_width(2)));
-  }
-#endif
-  *lds = q + (kp.lstack_on ? kLdsStackBytes : 0) + (kp.leaf_on ? kLeafBufBytes : 0) +
+  *lds = q + (kp.lstack_on ? kLdsStackBytes : 0) +
          (lm == 3 ? flat : lm == 1 ? full : lm == 2 ? (size_t)kp.S.ntop * node_bytes(lm_width(2)) : 0);
   return lm;
 }
@@ -795,7 +776,6 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   c->env_ntop_max = env_int("BDPT_NTOP_MAX", -1);
   c->block_major = env_int("BDPT_BLOCK_MAJOR", 1);
   c->xcd = env_int("BDPT_XCD_GROUPS", 0);
-  c->glds = env_int("BDPT_GLDS", 0);
   if (c->env_lds_mode > 3) { g_err = "BDPT_LDS_MODE must be 0..3"; delete c; return BDPT_E_INVALID; }
   c->pt = p.integrator == BDPT_INTEGRATOR_PT;
   if (p.integrator != BDPT_INTEGRATOR_BDPT && !c->pt) { g_err = "unknown integrator"; delete c; return BDPT_E_INVALID; }
@@ -906,7 +886,6 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
   kp.nmat = (int)c->hs.mats.size();
   kp.item_lo = 0;
   kp.lstack_on = 0;
-  kp.leaf_on = 0;
   kp.blocks = nullptr;
   kp.nbx = (W + 7) / 8;
   kp.nblocks = kp.nbx * ((H + 7) / 8);

@@ -39,7 +39,6 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.fn = flat_prims(hs, &S.fsph);
   S.ntop = 0;
   S.lstack = nullptr;
-  S.lleaf = nullptr;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
   S.env.light = hs.env_light;
@@ -160,7 +159,6 @@ extern "C" int core_cpu_pt_render(const bdpt_scene_desc* d, int W, int H, int sp
   S.fsph = 0;
   S.ntop = 0;
   S.lstack = nullptr;
-  S.lleaf = nullptr;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
   S.env.light = hs.env_light;
