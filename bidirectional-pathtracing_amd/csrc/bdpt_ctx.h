@@ -81,7 +81,8 @@ struct Ctx {
 inline SceneView view_of(const Ctx* c, int LM) {
   SceneView S;
   const int W = lm_width(LM);
-  S.nodes = (const float4*)(W == 4 ? c->d_nodes4 : c->d_nodes2);
+  // the device copy of the very tree the kernels of this width traverse (hs.tree(W))
+  S.nodes = (const float4*)(&c->hs.tree(W) == &c->hs.bvh4 ? c->d_nodes4 : c->d_nodes2);
   S.geom = (const float4*)c->d_geom;
   S.shade = (const float4*)c->d_shade;
   S.mats = c->d_mats;

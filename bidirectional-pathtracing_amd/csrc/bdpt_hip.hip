@@ -784,6 +784,16 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   }
   int rc = build_host_scene(scene, c->hs, g_err, c->pt);
   if (rc) { delete c; return rc; }
+  // host-side shape check before anything runs: each tree holds whole nodes of the stride its
+  // kernels read (hs.tree(lm_width(LM)) is what view_of hands the LDS mode LM)
+  for (int lm = 0; lm < 3; lm++) {
+    const int W = lm_width(lm);
+    if (c->hs.tree(W).nodes.size() % (4 * (size_t)node_f4(W)) != 0) {
+      g_err = "device tree layout does not match the kernels' node width";
+      delete c;
+      return BDPT_E_INVALID;
+    }
+  }
   c->ext = c->hs.env_light >= 0 || p.russian_roulette != 0;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {

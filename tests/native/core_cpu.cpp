@@ -31,13 +31,14 @@ static int run(const HostScene& hs, int W, int H, int spp, int M, uint64_t seed,
   S.nlights = (int)hs.lights.size();
   S.root = T.root;
   // LM 1 reads the "LDS copy": on the CPU the same arrays (exercises the LDS-mode tree)
-  S.lnodes = LM == 1 ? S.nodes : nullptr;
+  // LM 2 reads its BFS treelet [0, n_top) from the "LDS copy" (the same array on the CPU)
+  S.lnodes = LM == 1 || LM == 2 ? S.nodes : nullptr;
   S.lgeom = LM == 1 || LM == 3 ? S.geom : nullptr;
   S.lshade = LM == 3 ? S.shade : nullptr;
   S.lleaves = hs.leaf_refs.data();
   S.nleaves = (int)hs.leaf_refs.size();
   S.fn = flat_prims(hs, &S.fsph);
-  S.ntop = 0;
+  S.ntop = LM == 2 ? T.n_top : 0;
   S.lstack = nullptr;
   S.cam = hs.cam;
   const size_t np = (size_t)hs.env_w * hs.env_h;
@@ -104,11 +105,13 @@ static int render_lm(const bdpt_scene_desc* d, int W, int H, int spp, int M, uin
   return render_maxv<LM, false>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
 }
 
-// lds_mode 0: the HBM tree (lm_width(0) children per node); 1: the LDS-mode tree (lm_width(1))
+// lds_mode 0: the HBM tree (lm_width(0) children per node); 1: the LDS-mode tree (lm_width(1));
+// 2: the HBM tree with its BFS treelet read through the LDS path (same array on the CPU); 3: flat list
 extern "C" int core_cpu_render(const bdpt_scene_desc* d, int W, int H, int spp, int M, uint64_t seed, int s0,
                                int count, const int* pixels, int npix, double* eye, double* light, double* stats,
                                int lds_mode, int rr) {
   if (lds_mode == 1) return render_lm<1>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  if (lds_mode == 2) return render_lm<2>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   if (lds_mode == 3) return render_lm<3>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   return render_lm<0>(d, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
 }

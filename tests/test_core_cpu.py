@@ -121,17 +121,19 @@ def test_flat_list_is_one_run_of_primitives(name, n, nsph):
     assert bin(mask.value).count("1") == nsph
 
 
+@pytest.mark.parametrize("lds_mode", [0, 2])
 @pytest.mark.parametrize("scene,W,H,spp,M", [("scenes/CBbunny.dae", 64, 48, 2, 5),
                                              ("scenes/CBlucy_standin.dae", 48, 36, 2, 5)])
-def test_device_pipeline_bit_exact_mesh_trees(scene, W, H, spp, M):
+def test_device_pipeline_bit_exact_mesh_trees(scene, W, H, spp, M, lds_mode):
     """The 4-wide tree of a mesh scene (thousands of nodes; bvh.cpp:161-188 closest-hit semantics
     over a deep tree) vs mode 2: every padded child box must contain its primitives, or a hit goes
-    missing and the images differ."""
+    missing and the images differ. lds_mode 2 runs the north star's kernel path: the BFS treelet
+    read through the LDS node fetch (the same array on the CPU), the rest through the global one."""
     path = os.path.join(REPO, scene)
     if not os.path.exists(path):
         pytest.skip(f"{scene} not generated (tools/gen_standin.py, __graft_entry__.build)")
     sc = B.load_dae(path, W, H)
-    eye, light, st = core_render(sc, W, H, spp, M, seed=77, lds_mode=0)
+    eye, light, st = core_render(sc, W, H, spp, M, seed=77, lds_mode=lds_mode)
     _, oeye, olight, ost = oracle_render(sc, W, H, spp, M, MODE_C32, seed=77, threads=1)
     assert np.isfinite(eye).all() and np.isfinite(light).all()
     assert np.array_equal(eye, oeye), f"eye max diff {np.abs(eye - oeye).max()}"
