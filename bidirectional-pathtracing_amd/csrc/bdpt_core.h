@@ -466,6 +466,9 @@ BDPT_HD int* lane_stack(const SceneView& S) {
 #endif
 }
 
+#if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
+inline unsigned long long* step_hist() { static thread_local unsigned long long h[256]; return h; }
+#endif
 template <int K>
 struct TravStack {
   int s[K > 0 ? K : 1];
@@ -731,6 +734,14 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   TravStack<K> stk(stack_mem, LM == 1 || LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.closest++;
+#if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
+  // CPU diagnostics (tools/step_hist.py): the histogram of node steps per closest-hit query
+  struct StepHist {
+    const Counters& c;
+    uint32_t n0;
+    ~StepHist() { const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM); step_hist()[s < 255 ? s : 255]++; }
+  } step_hist_{c, c.nodes};
+#endif
   int li = 0;
   if (LM == 3 && S.fn > 0) {
     // the flat list as one run of primitives, the next record's loads issued before this test
