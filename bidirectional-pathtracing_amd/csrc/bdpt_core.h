@@ -467,7 +467,7 @@ BDPT_HD int* lane_stack(const SceneView& S) {
 }
 
 #if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
-inline unsigned long long* step_hist() { static thread_local unsigned long long h[256]; return h; }
+inline unsigned long long* step_hist() { static thread_local unsigned long long h[512]; return h; }
 #endif
 template <int K>
 struct TravStack {
@@ -867,6 +867,13 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   TravStack<K> stk(stack_mem, LM == 1 || LM == 2 ? lane_stack(S) : nullptr);
   int ref = S.root;
   c.shadow++;
+#if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
+  struct StepHistAny {   // any-hit queries: histogram entries 256..511
+    const Counters& c;
+    uint32_t n0;
+    ~StepHistAny() { const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM); step_hist()[256 + (s < 255 ? s : 255)]++; }
+  } step_hist_{c, c.nodes};
+#endif
   int li = 0;
   if (LM == 3 && S.fn > 0) {
     float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);

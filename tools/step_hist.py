@@ -42,14 +42,18 @@ for name, W, H, spp, M, lm in [("standin", 192, 108, 2, 5, 2), ("CBbunny", 160, 
     rc = lib.core_cpu_render(C.byref(d), W, H, spp, M, C.c_uint64(5489), 0, spp, None, 0, eye.ctypes.data_as(pd),
                              light.ctypes.data_as(pd), st.ctypes.data_as(pd), lm, 0)
     assert rc == 0
-    h = (C.c_ulonglong * 256)()
-    lib.core_cpu_step_hist(h)
-    h = np.array(h, dtype=np.float64)
+    hh = (C.c_ulonglong * 512)()
+    lib.core_cpu_step_hist(hh)
+    hh = np.array(hh, dtype=np.float64)
+    h, ha = hh[:256], hh[256:]
     n, k = h.sum(), np.arange(256)
     cdf = np.cumsum(h) / n
     emax = float(np.sum(1 - cdf[:255] ** 48))
+    cdfa = np.cumsum(ha) / max(1, ha.sum())
+    emaxa = float(np.sum(1 - cdfa[:255] ** 64))
     ref = oracle_render(sc, W, H, spp, M, MODE_C32, seed=5489, threads=8)
     exact = np.array_equal(eye, ref[1]) and np.array_equal(light, ref[2])
     print(f"{name} LM{lm}: steps/query mean {(h * k).sum() / n:.3f} p90 {int(np.searchsorted(cdf, .9))} "
           f"p99 {int(np.searchsorted(cdf, .99))} E[max of 48] {emax:.2f}; prim tests/query "
-          f"{(st[4] + st[5]) / max(1, st[1] + st[2]):.3f}; bit-exact vs mode 2: {exact}", flush=True)
+          f"{(st[4] + st[5]) / max(1, st[1] + st[2]):.3f}; any-hit steps/query mean "
+          f"{(ha * k).sum() / max(1, ha.sum()):.3f} E[max of 64] {emaxa:.2f}; bit-exact vs mode 2: {exact}", flush=True)
