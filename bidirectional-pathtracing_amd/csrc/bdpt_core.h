@@ -467,7 +467,8 @@ BDPT_HD int* lane_stack(const SceneView& S) {
 }
 
 #if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
-inline unsigned long long* step_hist() { static thread_local unsigned long long h[512]; return h; }
+inline unsigned long long* step_hist() { static thread_local unsigned long long h[1024]; return h; }
+inline int& step_hist_nested() { static thread_local int n = 0; return n; }
 #endif
 template <int K>
 struct TravStack {
@@ -739,7 +740,11 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   struct StepHist {
     const Counters& c;
     uint32_t n0;
-    ~StepHist() { const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM); step_hist()[s < 255 ? s : 255]++; }
+    ~StepHist() {
+      if (step_hist_nested()) return;
+      const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM);
+      step_hist()[s < 255 ? s : 255]++;
+    }
   } step_hist_{c, c.nodes};
 #endif
   int li = 0;
@@ -856,6 +861,20 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
     }
   }
   if (h.prim >= 0) c.hits++;
+#if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
+  // entries 512..767: node steps of the same query given its final hit distance up front (the
+  // ordering-independent part); 768..1023: node steps of the queries that hit nothing
+  if (!step_hist_nested()) {
+    step_hist_nested() = 1;
+    Counters c2 = {};
+    Hit h2;
+    trace_closest<LM, K>(S, o, d, tmin, h.prim >= 0 ? h.t * 1.000001f : tmax, h2, c2);
+    const uint32_t s2 = c2.nodes / (uint32_t)lm_width(LM);
+    step_hist()[512 + (s2 < 255 ? s2 : 255)]++;
+    if (h.prim < 0) step_hist()[768 + (s2 < 255 ? s2 : 255)]++;
+    step_hist_nested() = 0;
+  }
+#endif
   return h.prim >= 0;
 }
 
@@ -871,7 +890,11 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   struct StepHistAny {   // any-hit queries: histogram entries 256..511
     const Counters& c;
     uint32_t n0;
-    ~StepHistAny() { const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM); step_hist()[256 + (s < 255 ? s : 255)]++; }
+    ~StepHistAny() {
+      if (step_hist_nested()) return;
+      const uint32_t s = (c.nodes - n0) / (uint32_t)lm_width(LM);
+      step_hist()[256 + (s < 255 ? s : 255)]++;
+    }
   } step_hist_{c, c.nodes};
 #endif
   int li = 0;

@@ -205,7 +205,7 @@ extern "C" int core_cpu_dev_tree(const bdpt_scene_desc* d, int* depth, int* node
 
 #if defined(BDPT_STEP_HIST)
 // diagnostics (tools/step_hist.py): node steps per closest-hit query since the last call
-extern "C" void core_cpu_step_hist(unsigned long long* out512) {
-  for (int k = 0; k < 512; k++) { out512[k] = step_hist()[k]; step_hist()[k] = 0; }
+extern "C" void core_cpu_step_hist(unsigned long long* out1024) {
+  for (int k = 0; k < 1024; k++) { out1024[k] = step_hist()[k]; step_hist()[k] = 0; }
 }
 #endif

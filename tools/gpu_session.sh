@@ -5,6 +5,8 @@
 #                 and build_var_ph8.so (m <= 8), tools/build_variants.sh) on the north star and C5
 #   PART=bench    bench.py on WORKLOADS (default: ns c2 c3 c4 c5); ROCPROF=1 adds the rocprofv3
 #                 kernel stats of the default line
+#   PART=pmc      FETCH_SIZE / WRITE_SIZE passes per workload -> traffic_<w>.json, SQ / TCC groups
+#                 for WORKLOADS_SQ (default ns c5)
 #   PART=ab       A/B of variant libraries: LIBS="build_var_a.so build_var_b.so ..." on CFGS
 #                 (prof_render.py argument strings separated by ';'), ROUNDS interleaved rounds
 #   PART=full     tests, then bench
@@ -51,6 +53,37 @@ if [ "$PART" = ab ]; then
         step ab_r${r}_$(basename $lib .so)_$(echo $c | tr ' /.' '___') 300 env BDPT_LIB=$PWD/$lib $envx python3 tools/prof_render.py $a
       done
     done
+  done
+fi
+if [ "$PART" = pmc ]; then
+  # per workload: FETCH_SIZE and WRITE_SIZE passes (each with its kernel trace, so the bytes carry a
+  # duration) -> $OUT/<w>/traffic_<w>.json; then the SQ / TCC groups for WORKLOADS_SQ. One rocprofv3
+  # run per counter group (never combined with tracing domains), each under its own time limit.
+  declare -A ARGS=([ns]="scenes/CBlucy_standin.dae 1920 1080 128 5 1" [c2]="scenes/CBspheres.dae 480 360 128 5 1"
+    [c3]="scenes/CBlucy_standin.dae 800 600 128 5 1" [c4]="scenes/CBgems.dae 1920 1080 256 7 1"
+    [c5]="scenes/CBlucy_standin.dae 1920 1080 1024 8 1")
+  declare -A DESC=([ns]="CBlucy stand-in 1920x1080 s128 m5" [c2]="CBspheres 480x360 s128 m5"
+    [c3]="CBlucy stand-in 800x600 s128 m5" [c4]="CBgems 1920x1080 s256 m7"
+    [c5]="CBlucy stand-in + synthetic 1024x512 sky 1920x1080 s1024 m8 RR")
+  envs() { if [ "$1" = c5 ]; then export BDPT_ENV=synth:1024x512 BDPT_RR=1; else unset BDPT_ENV BDPT_RR; fi; }
+  for w in ${WORKLOADS:-ns c2 c3 c4 c5}; do
+    mkdir -p $OUT/$w
+    envs $w
+    step pmc_fetch_$w 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/$w/pmc_fetch -o run -- python3 tools/prof_render.py ${ARGS[$w]}
+    step pmc_write_$w 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/$w/pmc_write -o run -- python3 tools/prof_render.py ${ARGS[$w]}
+    step traffic_$w 60 python3 tools/pmc_traffic.py $OUT/$w $w "${DESC[$w]}, one launch (tools/prof_render.py)"
+  done
+  for w in ${WORKLOADS_SQ:-ns c5}; do
+    envs $w
+    i=0
+    for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+               "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_THREAD_CYCLES_VALU" \
+               "TCC_HIT_sum TCC_MISS_sum"; do
+      i=$((i+1))
+      step sq${i}_$w 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/$w/sq$i -o run -- python3 tools/prof_render.py ${ARGS[$w]}
+    done
+    python3 tools/pmc_summary.py $OUT/$w/sq1 $OUT/$w/sq2 $OUT/$w/sq3 > $OUT/pmc_$w.txt
+    cat $OUT/pmc_$w.txt
   done
 fi
 if [ "$PART" = bench ] || [ "$PART" = full ]; then

@@ -42,10 +42,10 @@ for name, W, H, spp, M, lm in [("standin", 192, 108, 2, 5, 2), ("CBbunny", 160, 
     rc = lib.core_cpu_render(C.byref(d), W, H, spp, M, C.c_uint64(5489), 0, spp, None, 0, eye.ctypes.data_as(pd),
                              light.ctypes.data_as(pd), st.ctypes.data_as(pd), lm, 0)
     assert rc == 0
-    hh = (C.c_ulonglong * 512)()
+    hh = (C.c_ulonglong * 1024)()
     lib.core_cpu_step_hist(hh)
     hh = np.array(hh, dtype=np.float64)
-    h, ha = hh[:256], hh[256:]
+    h, ha, ho, hm = hh[:256], hh[256:512], hh[512:768], hh[768:]
     n, k = h.sum(), np.arange(256)
     cdf = np.cumsum(h) / n
     emax = float(np.sum(1 - cdf[:255] ** 48))
@@ -57,3 +57,7 @@ for name, W, H, spp, M, lm in [("standin", 192, 108, 2, 5, 2), ("CBbunny", 160, 
           f"p99 {int(np.searchsorted(cdf, .99))} E[max of 48] {emax:.2f}; prim tests/query "
           f"{(st[4] + st[5]) / max(1, st[1] + st[2]):.3f}; any-hit steps/query mean "
           f"{(ha * k).sum() / max(1, ha.sum()):.3f} E[max of 64] {emaxa:.2f}; bit-exact vs mode 2: {exact}", flush=True)
+    cdfo = np.cumsum(ho) / max(1, ho.sum())
+    print(f"  given the final hit distance: mean {(ho * k).sum() / max(1, ho.sum()):.3f} p99 "
+          f"{int(np.searchsorted(cdfo, .99))} E[max of 48] {float(np.sum(1 - cdfo[:255] ** 48)):.2f}; queries that "
+          f"hit nothing: {hm.sum() / max(1, n):.3%} of all, their mean {(hm * k).sum() / max(1, hm.sum()):.2f}", flush=True)
