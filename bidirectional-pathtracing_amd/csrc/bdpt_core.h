@@ -415,6 +415,7 @@ static_assert((kBvhWidth == 2 || kBvhWidth == 4) && (kLdsBvhWidth == 2 || kLdsBv
 // Child visiting order of the 4-wide node step: 0 = slot order (any-hit connection rays),
 // 1 = near-first by a sorting network (closest-hit queries).
 constexpr int kAnyOrd = 0, kClosestOrd = 1;
+
 // BVH leaves: the next primitive's record is loaded before the current one is tested, where the
 // geometry comes from HBM (LM 0 / 2). Measured: Lucy stand-in 1080p 489 -> 516, CBbunny 800x600
 // 351 -> 370 Msamples/s; with the geometry in LDS (LM 1, CBgems) 303 -> 299, so off there. LM 3
@@ -520,16 +521,30 @@ struct TravStack {
 
 struct RayInv {
   f3 o, d, inv, oi;   // oi = o * inv: slab planes are fma(p, inv, -oi)
+  // 4-wide nodes: byte offset (0 or 16) of each axis' near plane row within its lo / hi row pair
+  // (the hi row when the direction component is negative), so that a lane loads its near and far
+  // rows directly and the per-axis min / max of the two plane distances disappears
+  int nx, ny, nz;
 };
+// A zero direction component would give an infinite inverse and NaN / wrong-signed plane distances
+// (inf - inf); it is replaced by +-2^-100, whose plane distances are huge and of the right sign, so a
+// parallel ray is inside a slab exactly when its origin is (up to the boxes' padding).
+BDPT_HD float safe_inv(float x) {
+  const float tiny = 7.88860905e-31f;   // 2^-100
+  return 1.0f / (fabsf(x) < tiny ? copysignf(tiny, x) : x);
+}
 BDPT_HD RayInv make_rayinv(f3 o, f3 d) {
   RayInv r;
   r.o = o; r.d = d;
-  r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.inv = mk3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   r.oi = mk3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+  r.nx = r.inv.x < 0.0f ? 16 : 0;
+  r.ny = r.inv.y < 0.0f ? 16 : 0;
+  r.nz = r.inv.z < 0.0f ? 16 : 0;
   return r;
 }
-// Slab test against a padded (conservative) box. NaN lanes (0 * inf) are ignored by fmin/fmax.
-// The fused form rounds differently from (p - o) * inv by at most ulp(o * inv) in t, far inside
+// Slab test against a padded (conservative) box (2-wide nodes; 4-wide nodes load the near and far
+// rows directly, node_step). The fused form rounds differently from (p - o) * inv by at most ulp(o * inv) in t, far inside
 // the 2^-16 box padding, so it never culls a box a hit lies in (results do not depend on it).
 BDPT_HD void slab(const RayInv& r, float lx, float ly, float lz_, float hx, float hy, float hz,
                   float* tn, float* tf) {
@@ -577,47 +592,53 @@ BDPT_HD int ld_lds_i(const int* p) {
   return *p;
 #endif
 }
-// A node from the LDS copy: one asm block of ds_read_b128 and a single wait. Written out because a
-// node fetch that may come from LDS or HBM (treelet mode) otherwise compiles to flat_load for both.
-template <int W>
-BDPT_HD void ld_node_lds(const float4* p, float4* v) {
+// A 4-wide node's rows as the ray sees them: v[0] / v[1] = the x plane rows nearer / farther along
+// the ray (lo.x / hi.x, swapped when the direction's x is negative), v[2] / v[3] y, v[4] / v[5] z,
+// v[6] the child references. Byte offsets within the node: near = 32 a + n_a, far = 32 a + 16 - n_a.
+BDPT_HD void ld_node4_oct_glb(const float4* p, const RayInv& r, float4* v) {
+  const char* b = (const char*)p;
+  const int nx = r.nx, ny = r.ny, nz = r.nz;
+  v[0] = ld_glb4((const float4*)(b + nx));
+  v[1] = ld_glb4((const float4*)(b + 16 - nx));
+  v[2] = ld_glb4((const float4*)(b + 32 + ny));
+  v[3] = ld_glb4((const float4*)(b + 48 - ny));
+  v[4] = ld_glb4((const float4*)(b + 64 + nz));
+  v[5] = ld_glb4((const float4*)(b + 80 - nz));
+  v[6] = ld_glb4((const float4*)(b + 96));
+}
+// the same from the LDS copy
+BDPT_HD void ld_node4_oct_lds(const float4* p, const RayInv& r, float4* v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef float v4f __attribute__((ext_vector_type(4)));
   const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)p;
+  const int nx = r.nx, ny = r.ny, nz = r.nz;
   v4f t[7];
-  if (node_used_f4(W) == 7) {
-    asm volatile(
-        "ds_read_b128 %0, %7\n\t"
-        "ds_read_b128 %1, %7 offset:16\n\t"
-        "ds_read_b128 %2, %7 offset:32\n\t"
-        "ds_read_b128 %3, %7 offset:48\n\t"
-        "ds_read_b128 %4, %7 offset:64\n\t"
-        "ds_read_b128 %5, %7 offset:80\n\t"
-        "ds_read_b128 %6, %7 offset:96\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
-        : "v"(a));
-  } else {
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:16\n\t"
-        "ds_read_b128 %2, %4 offset:32\n\t"
-        "ds_read_b128 %3, %4 offset:48\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
-        : "v"(a));
-  }
+  // one asm block of ds_read_b128 and a single wait (a node fetch that may come from LDS or HBM, as in
+  // the treelet mode, otherwise compiles to flat_load for both): near rows at a + n + 32 axis, far
+  // rows at a - n + 32 axis + 16
+  asm volatile(
+      "ds_read_b128 %0, %7\n\t"
+      "ds_read_b128 %1, %8 offset:16\n\t"
+      "ds_read_b128 %2, %9 offset:32\n\t"
+      "ds_read_b128 %3, %10 offset:48\n\t"
+      "ds_read_b128 %4, %11 offset:64\n\t"
+      "ds_read_b128 %5, %12 offset:80\n\t"
+      "ds_read_b128 %6, %13 offset:96\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
+      : "v"(a + nx), "v"(a - nx), "v"(a + ny), "v"(a - ny), "v"(a + nz), "v"(a - nz), "v"(a));
 #pragma unroll
-  for (int k = 0; k < node_used_f4(W); k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
+  for (int k = 0; k < 7; k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
 #else
-  for (int k = 0; k < node_used_f4(W); k++) v[k] = p[k];
+  ld_node4_oct_glb(p, r, v);
 #endif
 }
 
 // One node of the descent: slab-test the children, continue with the nearest hit child, push the
 // other hit children (farther first, so they pop near-first); pop when none is hit.
 // Width 2, 4 float4: lo_l.xyz hi_l.x | hi_l.yz lo_r.xy | lo_r.z hi_r.xyz | refs
-// Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad
+// Width 4, 8 float4: lo.x[4] | hi.x[4] | lo.y[4] | hi.y[4] | lo.z[4] | hi.z[4] | refs[4] | pad,
+// fetched in near / far order per axis (ld_node4_oct_*)
 // ORD: visit hit children near-first (closest-hit queries); any-hit queries take them in slot order.
 // A child is entered when its slab interval, clipped to [tmin, tmax], is non-empty.
 template <int K, int LM, int ORD = 1>
@@ -625,29 +646,35 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
                       Counters& c) {
   constexpr int W = lm_width(LM), NU = node_used_f4(W);
   float4 v[NU];
-  if (LM == 1) {   // all nodes in LDS: plain ds_reads the compiler schedules
+  if (W == 4) {
+    // rows in near / far order (ld_node4_oct_*). LM 2: the treelet (LDS) and HBM lanes of one wave
+    // would run a lane-divergent if / else over the same registers — the global loads, a wait for
+    // them (the ds_reads would overwrite their registers), then the ds_reads: HBM latency + LDS
+    // latency. So only a wave whose lanes are all in the treelet reads LDS; any other wave fetches
+    // every lane's node from HBM (the treelet nodes are there too, and hot in L2).
+    if (LM == 2) {
+      const bool in_lds = ref < S.ntop;
+#if defined(__HIP_DEVICE_COMPILE__)
+      const bool all_lds = __ballot(in_lds) == __ballot(true);
+#else
+      const bool all_lds = in_lds;
+#endif
+      if (all_lds) {
+        ld_node4_oct_lds(S.lnodes + node_f4(W) * ref, r, v);
+        c.lnodes += W;
+      } else {
+        ld_node4_oct_glb(S.nodes + node_f4(W) * ref, r, v);
+      }
+    } else if (LM == 1) {
+      ld_node4_oct_lds(S.lnodes + node_f4(W) * ref, r, v);
+      c.lnodes += W;
+    } else {
+      ld_node4_oct_glb(S.nodes + node_f4(W) * ref, r, v);
+    }
+  } else if (LM == 1) {   // 2-wide, all nodes in LDS: plain ds_reads the compiler schedules
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_lds4(S.lnodes + node_f4(W) * ref + k);
     c.lnodes += W;
-  } else if (LM == 2) {
-    // Treelet (LDS) and HBM lanes in one wave: a lane-divergent if / else over the same registers
-    // runs the global loads, waits for them (the ds_reads would overwrite their registers), then
-    // the ds_reads — HBM latency + LDS latency. Here only a wave whose lanes are all in the treelet
-    // reads LDS; any other wave fetches every lane's node from HBM (the treelet nodes are there too,
-    // and hot in L2), one fetch latency either way.
-    const bool in_lds = ref < S.ntop;
-#if defined(__HIP_DEVICE_COMPILE__)
-    const bool all_lds = __ballot(in_lds) == __ballot(true);
-#else
-    const bool all_lds = in_lds;
-#endif
-    if (all_lds) {
-      ld_node_lds<W>(S.lnodes + node_f4(W) * ref, v);
-      c.lnodes += W;
-    } else {
-#pragma unroll
-      for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
-    }
   } else {
 #pragma unroll
     for (int k = 0; k < NU; k++) v[k] = ld_glb4(S.nodes + node_f4(W) * ref + k);
@@ -679,14 +706,27 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     const float4 lz = v[4 % NU], hz = v[5 % NU], e = v[6 % NU];
     r0 = __float_as_int(e.x); r1 = __float_as_int(e.y); r2 = __float_as_int(e.z); r3 = __float_as_int(e.w);
     float tf;
-    slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, &tn0, &tf);
+    // lx / ly / lz are the near rows, hx / hy / hz the far rows (ld_node4_oct_*): with a finite
+    // inverse the near plane's distance is the smaller of the two (the fma is monotone in the plane
+    // coordinate), so this is slab()'s test without its per-axis min / max — 6 fewer VALU per child,
+    // the same visits. Measured against slab() (profiles/r05l_ab_oct_rows.log): north star +0.3 %,
+    // C5-shaped +1.2 %, CBbunny +0.3 %, the stand-in with the tree in HBM (LM 0) +2.5 %.
+#define BDPT_SLAB_OCT(C, TN, TF)                                                             \
+  {                                                                                          \
+    TN = fmaxf(fmaxf(fmaf(lx.C, r.inv.x, -r.oi.x), fmaf(ly.C, r.inv.y, -r.oi.y)),            \
+               fmaf(lz.C, r.inv.z, -r.oi.z));                                                \
+    TF = fminf(fminf(fmaf(hx.C, r.inv.x, -r.oi.x), fmaf(hy.C, r.inv.y, -r.oi.y)),            \
+               fmaf(hz.C, r.inv.z, -r.oi.z)) * 1.00000024f;                                  \
+  }
+    BDPT_SLAB_OCT(x, tn0, tf);
     h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
-    slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, &tn1, &tf);
+    BDPT_SLAB_OCT(y, tn1, tf);
     h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
-    slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, &tn2, &tf);
+    BDPT_SLAB_OCT(z, tn2, tf);
     h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
-    slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, &tn3, &tf);
+    BDPT_SLAB_OCT(w, tn3, tf);
     h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
+#undef BDPT_SLAB_OCT
     if (ORD == 0) {
       // continue with the lowest hit slot, push the others
       int nx = kTravDone;
@@ -992,61 +1032,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       if (LM != 3 && !stk.pop(ref)) return false;
     }
   }
-}
-
-// Resumable forms of the two queries for lane-refill loops: one call = descend to a leaf + test
-// it (same visit order, same results as trace_closest / trace_any); true when the query is done.
-// one leaf visit of a closest-hit query: descend to a leaf, test it; true when finished
-template <int LM, int K>
-BDPT_HD bool closest_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, Hit& h,
-                                             int& ref, TravStack<K>& stk, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
-  if (ref == kTravDone) return true;
-  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-  for (int k = 0; k < cnt; k++) {
-    const int pi = st + k;
-    float t, b1 = 0, b2 = 0;
-    bool ok;
-    int key;
-    if ((sm >> k) & 1) {
-      c.sphs++;
-      ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, h.t, &t);
-      key = ok ? __float_as_int(ld_geom<LM>(S, 3 * pi + 1).x) : 0;
-    } else {
-      c.tris++;
-      const float4 g2 = ld_geom<LM>(S, 3 * pi + 2);
-      ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), g2, o, d, tmin, h.t, &t, &b1, &b2);
-      key = __float_as_int(g2.y);
-    }
-    if (ok && (t < h.t || key > h.key)) {   // same rule as trace_closest (bdpt_core.h)
-      h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
-    }
-  }
-  return !stk.pop(ref);
-}
-
-// one leaf visit of an any-hit query: true when finished (*hit tells whether something was hit)
-template <int LM, int K>
-BDPT_HD bool any_step(const SceneView& S, const RayInv& r, f3 o, f3 d, float tmin, float tmax,
-                                         int& ref, TravStack<K>& stk, bool* hit, Counters& c) {
-  while (ref >= 0) ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
-  if (ref == kTravDone) { *hit = false; return true; }
-  const int st = leaf_start(ref), cnt = leaf_count(ref), sm = leaf_sph_mask(ref);
-  for (int k = 0; k < cnt; k++) {
-    const int pi = st + k;
-    float t, b1, b2;
-    bool ok;
-    if ((sm >> k) & 1) {
-      c.sphs++;
-      ok = sph_test(ld_geom<LM>(S, 3 * pi), o, d, tmin, tmax, &t);
-    } else {
-      c.tris++;
-      ok = tri_test(ld_geom<LM>(S, 3 * pi), ld_geom<LM>(S, 3 * pi + 1), ld_geom<LM>(S, 3 * pi + 2), o, d, tmin, tmax, &t, &b1, &b2);
-    }
-    if (ok) { *hit = true; return true; }
-  }
-  if (!stk.pop(ref)) { *hit = false; return true; }
-  return false;
 }
 
 // Shading record of a closest hit: interpolated normal (triangle.cpp:80-82) or sphere normal

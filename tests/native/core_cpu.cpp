@@ -203,6 +203,79 @@ extern "C" int core_cpu_dev_tree(const bdpt_scene_desc* d, int* depth, int* node
   return 0;
 }
 
+// Closest hits of the device traversal (lds_mode 0, 1 or 2) against a brute-force loop over every
+// primitive with the same tests and tie rule, for n rays with origins spread over the scene's box and
+// directions with exact zero (and -0) components: axis-aligned and in the coordinate planes (a zero
+// component once gave an infinite inverse and NaN / -inf plane distances, bdpt_core.h safe_inv).
+// Returns the number of rays whose hit (primitive, t) differs; *hits = rays that hit something.
+template <int LM>
+static int trace_check_lm(const HostScene& hs, int n, uint64_t seed, int* hits) {
+  SceneView S = {};
+  const HostBvh& T = hs.tree(lm_width(LM));
+  S.nodes = (const float4*)T.nodes.data();
+  S.geom = (const float4*)hs.geom.data();
+  S.shade = (const float4*)hs.shade.data();
+  S.root = T.root;
+  S.lnodes = LM == 1 || LM == 2 ? S.nodes : nullptr;
+  S.lgeom = LM == 1 ? S.geom : nullptr;
+  S.ntop = LM == 2 ? T.n_top : 0;
+  const int np = (int)(hs.geom.size() / 12);
+  float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+  for (int i = 0; i < np; i++) {
+    const float* g = &hs.geom[12 * i];
+    const bool sph = __float_as_int(hs.shade[12 * i + 10]) != 0;
+    for (int v = 0; v < (sph ? 1 : 3); v++)
+      for (int k = 0; k < 3; k++) {
+        const float e = v == 0 ? 0.0f : (v == 1 ? g[3 + k] : g[6 + k]);
+        const float x = g[k] + e;
+        lo[k] = fminf(lo[k], x); hi[k] = fmaxf(hi[k], x);
+      }
+  }
+  uint64_t st = seed;
+  auto rnd = [&]() { st = st * 6364136223846793005ull + 1442695040888963407ull; return (float)((st >> 40) & 0xffffff) / 16777216.0f; };
+  int bad = 0;
+  *hits = 0;
+  Counters cnt = {};
+  for (int q = 0; q < n; q++) {
+    f3 o = mk3(lo[0] + (hi[0] - lo[0]) * rnd(), lo[1] + (hi[1] - lo[1]) * rnd(), lo[2] + (hi[2] - lo[2]) * rnd());
+    float dv[3] = {rnd() * 2 - 1, rnd() * 2 - 1, rnd() * 2 - 1};
+    const int pat = q % 7;   // which components are zeroed: one axis (3), two axes (3), none
+    if (pat < 3) dv[pat] = (q & 8) ? -0.0f : 0.0f;
+    else if (pat < 6) { dv[(pat + 1) % 3] = 0.0f; dv[(pat + 2) % 3] = (q & 8) ? -0.0f : 0.0f; }
+    f3 d = normalize(mk3(dv[0], dv[1], dv[2]));
+    if (!(norm2(d) > 0.5f)) continue;
+    Hit h;
+    trace_closest<LM, kWalkStack>(S, o, d, 1e-5f, 1e30f, h, cnt);
+    float bt = 1e30f;
+    int bp = -1, bk = -1;
+    for (int i = 0; i < np; i++) {
+      const float4* g = S.geom + 3 * i;
+      float t, b1, b2;
+      bool ok;
+      int key;
+      if (__float_as_int(hs.shade[12 * i + 10]) != 0) {
+        ok = sph_test(g[0], o, d, 1e-5f, bt, &t);
+        key = __float_as_int(g[1].x);
+      } else {
+        ok = tri_test(g[0], g[1], g[2], o, d, 1e-5f, bt, &t, &b1, &b2);
+        key = __float_as_int(g[2].y);
+      }
+      if (ok && (t < bt || key > bk)) { bt = t; bp = i; bk = key; }
+    }
+    if (bp >= 0) (*hits)++;
+    if (bp != h.prim || (bp >= 0 && bt != h.t)) bad++;
+  }
+  return bad;
+}
+
+extern "C" int core_cpu_trace_check(const bdpt_scene_desc* d, int lds_mode, int n, uint64_t seed, int* hits) {
+  HostScene hs;
+  std::string err;
+  if (build_host_scene(d, hs, err) != BDPT_OK) return -1;
+  if (lds_mode == 1) return trace_check_lm<1>(hs, n, seed, hits);
+  return lds_mode == 2 ? trace_check_lm<2>(hs, n, seed, hits) : trace_check_lm<0>(hs, n, seed, hits);
+}
+
 #if defined(BDPT_STEP_HIST)
 // diagnostics (tools/step_hist.py): node steps per closest-hit query since the last call
 extern "C" void core_cpu_step_hist(unsigned long long* out1024) {
