@@ -209,7 +209,7 @@ extern "C" int core_cpu_dev_tree(const bdpt_scene_desc* d, int* depth, int* node
 // component once gave an infinite inverse and NaN / -inf plane distances, bdpt_core.h safe_inv).
 // Returns the number of rays whose hit (primitive, t) differs; *hits = rays that hit something.
 template <int LM>
-static int trace_check_lm(const HostScene& hs, int n, uint64_t seed, int* hits) {
+static SceneView trace_view(const HostScene& hs) {
   SceneView S = {};
   const HostBvh& T = hs.tree(lm_width(LM));
   S.nodes = (const float4*)T.nodes.data();
@@ -219,6 +219,12 @@ static int trace_check_lm(const HostScene& hs, int n, uint64_t seed, int* hits) 
   S.lnodes = LM == 1 || LM == 2 ? S.nodes : nullptr;
   S.lgeom = LM == 1 ? S.geom : nullptr;
   S.ntop = LM == 2 ? T.n_top : 0;
+  return S;
+}
+
+template <int LM>
+static int trace_check_lm(const HostScene& hs, int n, uint64_t seed, int* hits) {
+  const SceneView S = trace_view<LM>(hs);
   const int np = (int)(hs.geom.size() / 12);
   float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
   for (int i = 0; i < np; i++) {
@@ -274,6 +280,39 @@ extern "C" int core_cpu_trace_check(const bdpt_scene_desc* d, int lds_mode, int 
   if (build_host_scene(d, hs, err) != BDPT_OK) return -1;
   if (lds_mode == 1) return trace_check_lm<1>(hs, n, seed, hits);
   return lds_mode == 2 ? trace_check_lm<2>(hs, n, seed, hits) : trace_check_lm<0>(hs, n, seed, hits);
+}
+
+// bdpt_trace_rays (k_trace_rays) on the CPU: rays = n x (o, d, tmin, tmax); closest hit t and the
+// primitive's scene index (-1: none), or for any_hit whether anything lies in [tmin, tmax]
+template <int LM>
+static void trace_rays_lm(const HostScene& hs, const float* rays, int n, int any_hit, float* out_t, int* out_prim) {
+  const SceneView S = trace_view<LM>(hs);
+  Counters c = {};
+  for (int i = 0; i < n; i++) {
+    const float* r = rays + 8 * (size_t)i;
+    const f3 o = mk3(r[0], r[1], r[2]), d = mk3(r[3], r[4], r[5]);
+    if (any_hit) {
+      const bool h = trace_any<LM, kConnStack>(S, o, d, r[6], r[7], c);
+      out_t[i] = h ? 0.0f : INFINITY;
+      out_prim[i] = h ? 0 : -1;
+    } else {
+      Hit h;
+      const bool ok = trace_closest<LM, kWalkStack>(S, o, d, r[6], r[7], h, c);
+      out_t[i] = ok ? h.t : INFINITY;
+      out_prim[i] = ok ? hs.prim_ref[h.prim] : -1;
+    }
+  }
+}
+
+extern "C" int core_cpu_trace_rays(const bdpt_scene_desc* d, int lds_mode, const float* rays, int n, int any_hit,
+                                   float* out_t, int* out_prim) {
+  HostScene hs;
+  std::string err;
+  if (build_host_scene(d, hs, err) != BDPT_OK) return -1;
+  if (lds_mode == 1) trace_rays_lm<1>(hs, rays, n, any_hit, out_t, out_prim);
+  else if (lds_mode == 2) trace_rays_lm<2>(hs, rays, n, any_hit, out_t, out_prim);
+  else trace_rays_lm<0>(hs, rays, n, any_hit, out_t, out_prim);
+  return 0;
 }
 
 #if defined(BDPT_STEP_HIST)

@@ -218,3 +218,56 @@ def test_traversal_with_zero_direction_components_matches_brute_force(name, lds_
                                    C.byref(hits))
     assert bad == 0
     assert hits.value > 500
+
+
+def zero_component_rays(n, seed, lo, hi):
+    """n rays (o, d, tmin, tmax) from origins uniform in [lo, hi] whose directions have exact 0 / -0
+    components: one axis zeroed, two axes zeroed (axis-aligned), and none, in turn."""
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    k = np.arange(n)
+    sign = np.where(k % 16 >= 8, np.float32(-0.0), np.float32(0.0))
+    for a in range(3):
+        d[k % 7 == a, a] = sign[k % 7 == a]
+        two = k % 7 == 3 + a
+        d[two, (a + 1) % 3] = 0.0
+        d[two, (a + 2) % 3] = sign[two]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d, np.full((n, 1), 1e-5, np.float32), np.full((n, 1), np.inf, np.float32)],
+                          axis=1).astype(np.float32)
+
+
+def zero_ray_scene(name):
+    if name == "CBbunny":
+        return B.load_dae(os.path.join(REPO, "scenes", "CBbunny.dae"), 32, 24), (-0.9, 0.05, -0.9), (0.9, 1.4, 0.9)
+    return golden_scene(name, 32, 24), (-0.9, 0.05, -0.9), (0.9, 1.4, 0.9)
+
+
+@pytest.mark.parametrize("lds_mode", [0, 1, 2])
+@pytest.mark.parametrize("name", ["CBbunny", "CBgems"])
+def test_zero_component_rays_match_oracle(name, lds_mode):
+    """The same rays through bdpt_trace_rays' traversal (CPU build) and the oracle's mode-2 tracer
+    (the reference's BVH and BBox::intersect, fp32): identical closest-hit primitives and t, and
+    any-hit agrees with them (the GPU side: tests/test_gpu_parity.py)."""
+    from _util import oracle
+    sc, lo, hi = zero_ray_scene(name)
+    n = 3000
+    rays = zero_component_rays(n, 11, lo, hi)
+    lib = core()
+    lib.core_cpu_trace_rays.argtypes = [C.POINTER(B.SceneDesc), C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int,
+                                        C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    d_ = sc.desc()
+    PF, PI = C.POINTER(C.c_float), C.POINTER(C.c_int)
+    t, p, ta, pa, ot, op = (np.empty(n, np.float32), np.empty(n, np.int32), np.empty(n, np.float32),
+                            np.empty(n, np.int32), np.empty(n, np.float32), np.empty(n, np.int32))
+    assert lib.core_cpu_trace_rays(C.byref(d_), lds_mode, rays.ctypes.data_as(PF), n, 0, t.ctypes.data_as(PF),
+                                   p.ctypes.data_as(PI)) == 0
+    assert lib.core_cpu_trace_rays(C.byref(d_), lds_mode, rays.ctypes.data_as(PF), n, 1, ta.ctypes.data_as(PF),
+                                   pa.ctypes.data_as(PI)) == 0
+    oracle().oracle_trace_rays(C.byref(d_), 2, rays.ctypes.data_as(PF), n, 0, ot.ctypes.data_as(PF),
+                               op.ctypes.data_as(PI))
+    assert (op >= 0).sum() > n // 2
+    assert np.array_equal(p, op)
+    assert np.array_equal(t[op >= 0], ot[op >= 0])
+    assert np.array_equal(pa >= 0, op >= 0)

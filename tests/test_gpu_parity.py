@@ -136,6 +136,34 @@ def test_trace_rays_matches_oracle():
     assert np.array_equal(np.isfinite(ta), op >= 0)
 
 
+@pytest.mark.parametrize("name", ["CBbunny", "CBgems"])
+def test_trace_rays_zero_direction_components_match_oracle(name):
+    """Rays with exact 0 / -0 direction components (axis-aligned, in coordinate planes) through the
+    device traversal: the same closest hits as the oracle's mode-2 tracer, any-hit agreeing. The
+    traversal before round 5's safe_inv culled boxes such rays run through inside a slab
+    (tests/test_core_cpu.py has the CPU-build and brute-force checks)."""
+    from test_core_cpu import zero_component_rays, zero_ray_scene
+    sc, lo, hi = zero_ray_scene(name)
+    n = 3000
+    rays = zero_component_rays(n, 11, lo, hi)
+    pt = B.BidirectionalPathTracer(sc, 32, 24, 1, 5)
+    try:
+        t, prim = pt.trace_rays(rays, any_hit=False)
+        ta, _ = pt.trace_rays(rays, any_hit=True)
+    finally:
+        pt.close()
+    ot = np.empty(n, np.float32)
+    op = np.empty(n, np.int32)
+    d_ = sc.desc()
+    oracle().oracle_trace_rays(C.byref(d_), 2, rays.ctypes.data_as(C.POINTER(C.c_float)), n, 0,
+                               ot.ctypes.data_as(C.POINTER(C.c_float)),
+                               op.ctypes.data_as(C.POINTER(C.c_int)))
+    assert (op >= 0).sum() > n // 2
+    assert np.array_equal(prim, op)
+    assert np.array_equal(t[op >= 0], ot[op >= 0])
+    assert np.array_equal(np.isfinite(ta), op >= 0)
+
+
 def test_unsupported_material_rejected():
     sc = golden_scene("CBspheres", 32, 24)
     sc.mats[0].type = B.MAT_MICROFACET
