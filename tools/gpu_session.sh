@@ -9,6 +9,7 @@
 #                 for WORKLOADS_SQ (default ns c5)
 #   PART=ab       A/B of variant libraries: LIBS="build_var_a.so build_var_b.so ..." on CFGS
 #                 (prof_render.py argument strings separated by ';'), ROUNDS interleaved rounds
+#   PART=pt       bench.py --integrator pt (the PathTracer) on ns, c2, a microfacet scene, bunny.dae
 #   PART=full     tests, then bench
 # Every GPU step runs under its own timeout; the script stops at the first abort / fault / timeout.
 cd "$(dirname "$0")/.." || exit 1
@@ -85,6 +86,16 @@ if [ "$PART" = pmc ]; then
     python3 tools/pmc_summary.py $OUT/$w/sq1 $OUT/$w/sq2 $OUT/$w/sq3 > $OUT/pmc_$w.txt
     cat $OUT/pmc_$w.txt
   done
+fi
+if [ "$PART" = pt ]; then
+  # the unidirectional PathTracer on the BDPT workloads' scenes and the ones only it renders
+  step bench_pt_ns 600 python bench.py --integrator pt --workload ns --steps 3 --warmup 1 --no-cpu-baseline
+  step bench_pt_c2 600 python bench.py --integrator pt --workload c2 --steps 3 --warmup 1 --no-cpu-baseline
+  step bench_pt_mf 600 python bench.py --integrator pt --scene scenes/CBspheres_microfacet_al_ag.dae --steps 3 --warmup 1 --no-cpu-baseline
+  step bench_pt_bunny 600 python bench.py --integrator pt --scene scenes/bunny.dae --steps 3 --warmup 1 --no-cpu-baseline
+  if [ -n "$ROCPROF" ]; then
+    step rocprof_pt 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_pt -o run -- python3 bench.py --integrator pt --steps 3 --warmup 1 --no-cpu-baseline --no-parity
+  fi
 fi
 if [ "$PART" = bench ] || [ "$PART" = full ]; then
   for w in ${WORKLOADS:-ns c2 c3 c4 c5}; do
