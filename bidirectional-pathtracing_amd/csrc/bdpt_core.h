@@ -468,8 +468,13 @@ BDPT_HD int* lane_stack(const SceneView& S) {
 }
 
 #if defined(BDPT_STEP_HIST) && !defined(__HIP_DEVICE_COMPILE__)
+}  // namespace bdpt
+#include <vector>
+namespace bdpt {
 inline unsigned long long* step_hist() { static thread_local unsigned long long h[1024]; return h; }
 inline int& step_hist_nested() { static thread_local int n = 0; return n; }
+// diagnostics: the any-hit queries' rays (o, d, tmin, tmax) while a sink is set (tools/anyhit_probe.py)
+inline std::vector<float>*& ray_dump() { static thread_local std::vector<float>* v = nullptr; return v; }
 #endif
 template <int K>
 struct TravStack {
@@ -936,6 +941,10 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       step_hist()[256 + (s < 255 ? s : 255)]++;
     }
   } step_hist_{c, c.nodes};
+  if (ray_dump() && !step_hist_nested()) {
+    const float rv[8] = {o.x, o.y, o.z, d.x, d.y, d.z, tmin, tmax};
+    ray_dump()->insert(ray_dump()->end(), rv, rv + 8);
+  }
 #endif
   int li = 0;
   if (LM == 3 && S.fn > 0) {

@@ -316,6 +316,18 @@ extern "C" int core_cpu_trace_rays(const bdpt_scene_desc* d, int lds_mode, const
 }
 
 #if defined(BDPT_STEP_HIST)
+// diagnostics (tools/anyhit_probe.py): collect the any-hit rays of the following renders (max_rays,
+// 0 = stop), then copy up to max_rays of them out; returns the number collected
+static std::vector<float> g_rays;
+extern "C" void core_cpu_ray_dump(int on) {
+  g_rays.clear();
+  ray_dump() = on ? &g_rays : nullptr;
+}
+extern "C" long long core_cpu_ray_dump_get(float* out, long long max_rays) {
+  const long long n = std::min<long long>(max_rays, (long long)g_rays.size() / 8);
+  std::copy(g_rays.begin(), g_rays.begin() + 8 * n, out);
+  return (long long)g_rays.size() / 8;
+}
 // diagnostics (tools/step_hist.py): node steps per closest-hit query since the last call
 extern "C" void core_cpu_step_hist(unsigned long long* out1024) {
   for (int k = 0; k < 1024; k++) { out1024[k] = step_hist()[k]; step_hist()[k] = 0; }
