@@ -50,8 +50,10 @@ def core_render(scene, W, H, spp, M, seed=5489, s0=0, count=None, lds_mode=0, rr
 CASES = [("CBspheres", 32, 24, 2, 5), ("CBspheres_lambertian", 32, 24, 2, 5), ("CBgems", 32, 24, 1, 7),
          ("CBempty", 32, 24, 2, 5), ("CBspheres_refract", 24, 18, 2, 5), ("CBspheres", 24, 18, 1, 8),
          ("CBspheres", 24, 18, 3, 1),
-         # the m <= 32 kernel (64-bit delta masks): mirror / glass chains run long here
-         ("CBspheres", 24, 18, 2, 20), ("CBgems", 24, 18, 1, 32)]
+         # the m <= 32 and m <= 62 kernels (64-bit delta masks): mirror / glass chains run long here
+         ("CBspheres", 24, 18, 2, 20), ("CBgems", 24, 18, 1, 32),
+         # the m <= 62 kernel
+         ("CBspheres", 24, 18, 1, 62)]
 
 
 @pytest.mark.parametrize("lds_mode", [0, 1, 3])
@@ -70,7 +72,7 @@ def test_device_pipeline_bit_exact_vs_oracle_mode2(name, W, H, spp, M, lds_mode)
 EXT_CASES = [("CBspheres_lambertian", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 5, False, True),
              ("CBempty", 32, 24, 2, 5, False, True), ("CBspheres", 32, 24, 2, 8, True, False),
              ("CBgems", 32, 24, 1, 7, True, True), ("CBspheres_lambertian", 24, 18, 2, 8, True, True),
-             ("CBspheres", 24, 18, 2, 24, True, True),
+             ("CBspheres", 24, 18, 2, 24, True, True), ("CBspheres", 24, 18, 1, 50, True, True),
              # non-power-of-two map: the guide tables' cells (powers of two) straddle CDF entries
              ("CBspheres_lambertian", 24, 18, 4, 5, False, (37, 19))]
 
