@@ -141,7 +141,7 @@ typedef struct bdpt_params {
   int32_t width;              /* frame size (PathTracer::set_frame_size)                 */
   int32_t height;
   int32_t spp;                /* ns_aa: the 1/ns_aa weight of every sample                */
-  int32_t max_depth;          /* max_ray_depth (-m)                                      */
+  int32_t max_depth;          /* max_ray_depth (-m); BDPT: 0..62, PathTracer: 0..21      */
   uint64_t seed;
   int32_t samples_per_lane;   /* 0 = auto                                                 */
   int32_t device;             /* HIP device ordinal                                       */

@@ -273,3 +273,17 @@ def test_zero_component_rays_match_oracle(name, lds_mode):
     assert np.array_equal(p, op)
     assert np.array_equal(t[op >= 0], ot[op >= 0])
     assert np.array_equal(pa >= 0, op >= 0)
+
+
+@pytest.mark.parametrize("lds_mode", [0, 2])
+@pytest.mark.parametrize("name,M", [("CBbunny", 5), ("CBcoil", 5), ("CBcoil", 8), ("CBlucy_standin", 5)])
+def test_mesh_scenes_bit_exact_vs_oracle_mode2(name, M, lds_mode):
+    """The reference's mesh scenes under BDPT (scenes/*.dae through the product's loader): the CPU
+    build of the device pipeline is bit-exact against oracle mode 2 with the 4-wide tree in HBM (0)
+    and with its treelet read through the LDS path (2)."""
+    W, H, spp = 40, 30, 2
+    sc = B.load_dae(os.path.join(REPO, "scenes", name + ".dae"), W, H)
+    eye, light, _ = core_render(sc, W, H, spp, M, lds_mode=lds_mode)
+    _, oeye, olight, _ = oracle_render(sc, W, H, spp, M, MODE_C32, threads=8)
+    assert oeye.mean() + olight.mean() > 0
+    assert np.array_equal(eye, oeye) and np.array_equal(light, olight)

@@ -7,12 +7,13 @@ difference is the order of fp32 atomic additions of the light-image splats and o
 eye sums, ~1e-7 relative.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
 
 import bdpt_amd as B
-from _util import MODE_C32, golden_scene, oracle, oracle_render
+from _util import MODE_C32, REPO, golden_scene, oracle, oracle_render
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +66,23 @@ def test_parity_vs_oracle(name, W, H, S, M, pipe):
     rl = _rmse(g["light"], light)
     print(f"{name} {W}x{H} s{S} m{M}: rmse sample {r:.3e} eye {re:.3e} light {rl:.3e} "
           f"mean gpu {g['sample'].mean():.6f} oracle {samp.mean():.6f}")
+    assert r < RMSE_TOL and re < RMSE_TOL and rl < RMSE_TOL
+
+
+@pytest.mark.parametrize("lds", [None, 0])
+@pytest.mark.parametrize("name,M", [("CBbunny", 5), ("CBcoil", 5), ("CBcoil", 8)])
+def test_mesh_scene_parity_vs_oracle(name, M, lds, monkeypatch):
+    """The reference's mesh scenes that the BDPT integrator renders (scenes/*.dae loaded by the
+    product's loader) against oracle mode 2: the default LDS mode (treelet) and the tree in HBM."""
+    if lds is not None:
+        monkeypatch.setenv("BDPT_LDS_MODE", str(lds))
+    W, H, S = 96, 72, 2
+    sc = B.load_dae(os.path.join(REPO, "scenes", name + ".dae"), W, H)
+    g = _gpu_render(sc, W, H, S, M)
+    samp, eye, light, st = oracle_render(sc, W, H, S, M, MODE_C32)
+    r, re, rl = _rmse(g["sample"], samp), _rmse(g["eye"], eye), _rmse(g["light"], light)
+    print(f"{name} {W}x{H} s{S} m{M} lds {lds}: rmse sample {r:.3e} eye {re:.3e} light {rl:.3e}")
+    assert samp.mean() > 0
     assert r < RMSE_TOL and re < RMSE_TOL and rl < RMSE_TOL
 
 
