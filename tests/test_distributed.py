@@ -1,4 +1,4 @@
-"""The multi-GPU path on the CPU (gloo, world size 2): bdpt_amd.ShardedRender — the product's split
+"""The multi-GPU path on the CPU (gloo, world sizes 2 and 4): bdpt_amd.ShardedRender — the product's split
 of every pixel's sample range across the ranks (rank_sample_range: strong = one fixed render split,
 weak = a full spp per rank), the sample frame copied into a float32 tensor and ONE all-reduce of it
  — exactly as bench.py drives it over RCCL, with the renderer swapped for the
@@ -30,9 +30,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _spp(world):
+    """samples per pixel per step: one per rank at least under strong scaling"""
+    return max(S, world)
+
+
 def _total(world, scaling):
     """samples per pixel of the whole job (the ctx weight 1/ns_aa)"""
-    return STEPS * S if scaling == "strong" else STEPS * world * S
+    return STEPS * _spp(world) if scaling == "strong" else STEPS * world * _spp(world)
 
 
 class CoreCpuRenderer:
@@ -64,7 +69,8 @@ def _worker(rank, world, port, out_path, scaling):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = golden_scene("CBspheres", W, H)
     frame = torch.zeros(H * W * 3, dtype=torch.float32)
-    sh = B.ShardedRender(CoreCpuRenderer(sc, W, H, _total(world, scaling), M), frame, rank, world, S, scaling, dist)
+    sh = B.ShardedRender(CoreCpuRenderer(sc, W, H, _total(world, scaling), M), frame, rank, world, _spp(world),
+                         scaling, dist)
     for step in range(STEPS):
         sh.step(step)
     rows = sh.gather_floats([float(rank), float(W * H * sh.samples(0))], device="cpu")
@@ -74,16 +80,16 @@ def _worker(rank, world, port, out_path, scaling):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("scaling", ["strong", "weak"])
-def test_sharded_render_reduces_to_single_render(tmp_path, scaling):
+def test_sharded_render_reduces_to_single_render(tmp_path, scaling, world):
     from test_core_cpu import core_render
-    world = 2
     out = str(tmp_path / "reduced.npy")
     mp.spawn(_worker, args=(world, _free_port(), out, scaling), nprocs=world, join=True)
     reduced = np.load(out)
     rows = np.load(out + ".rows.npy")
-    assert rows[:, 0].tolist() == [0.0, 1.0]                  # every rank reported its row
-    per_rank = S // world if scaling == "strong" else S
+    assert rows[:, 0].tolist() == [float(r) for r in range(world)]   # every rank reported its row
+    per_rank = _spp(world) // world if scaling == "strong" else _spp(world)
     assert rows[:, 1].tolist() == [W * H * per_rank] * world
     sc = golden_scene("CBspheres", W, H)
     tot = _total(world, scaling)
