@@ -565,6 +565,7 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
       err = "BVH deeper than the traversal stack";
       return BDPT_E_UNSUPPORTED;
     }
+    bool wide_sph_leaf = false;
     auto ref_of = [&](int id) -> int {
       const Node& nd = T.nodes[id];
       if (nd.l >= 0) return dev_index[id];
@@ -573,6 +574,7 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
         int i = T.leaf_prims[nd.start + k];
         if (d->prim_type[i] == BDPT_PRIM_SPHERE) mask |= 1 << k;
       }
+      if (mask >> 4) wide_sph_leaf = true;   // the reference's sphere mask has 4 bits
       uint32_t enc = ((uint32_t)nd.start << 7) | ((uint32_t)mask << 3) | (uint32_t)nd.count;
       return (int)~enc;
     };
@@ -624,6 +626,10 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
         st.push_back(T.nodes[id].r);
         st.push_back(T.nodes[id].l);
       }
+    }
+    if (wide_sph_leaf) {
+      err = "a BVH leaf holds a sphere past its 4th primitive (the leaf reference's sphere mask has 4 bits)";
+      return BDPT_E_UNSUPPORTED;
     }
   }
   return BDPT_OK;
