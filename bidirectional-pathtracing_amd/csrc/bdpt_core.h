@@ -400,7 +400,9 @@ constexpr int kStackMax = 64;
 // Measured (Lucy stand-in 1080p / CBspheres / CBgems, Msamples/s): K 0: 440 / 438 / 273,
 // K 2: 465 / 452 / 284, K 4: 465 / 450 / 290 (walk 8 or connection 8: no further gain). Round 4,
 // with 8 LDS slots behind them (kLdsStack): walk / connection 2/2, 3/3, 2/4, 4/2 lose 0.6 .. 1.7 %
-// on the north star (profiles/r04k_ab_regstack.log).
+// on the north star (profiles/r04k_ab_regstack.log). Round 5, with the LDS slots: 0 / 0 and 0 / 4
+// -0.5 % on the north star, 4 / 0 +-0.2 %; with the tree in HBM (no LDS slots) 0 / 0 -10 %, and on
+// CBgems (LM 1) -2 % (profiles/r05y_ab_regstack.log).
 constexpr int kWalkStack = 4;
 constexpr int kConnStack = 4;
 // Children per BVH node: 2 (64-B nodes) or 4 (128-B nodes: half the dependent node fetches per
