@@ -155,13 +155,12 @@ constexpr int kMinWaves = 4;
 constexpr int kBlock = 256 * kMinWaves;   // one block per CU: one LDS scene copy shared by its 16 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 
-// Connections: general (i, j >= 2) pairs from per-lane compacted lists instead of the
-// wave-uniform max|E| x max|L| grid (the special strategies stay wave-uniform). 0 = never, 1 =
-// always, 2 = for the long-path kernels (MAXV >= 8, m > 5), where the grid is mostly empty: measured
-// C5-shaped (m8, env, RR) 446 -> 470, CBgems m7 +0.9%; the m5 north star -1.7% (so grid there).
-constexpr int kConnCompact = 2;
-template <int MAXV>
-constexpr bool conn_compact() { return kConnCompact == 1 || (kConnCompact == 2 && MAXV >= 8); }
+// Connections: every strategy from per-lane compacted lists (connect_sample) instead of the
+// wave-uniform max|E| x max|L| grid. History: the general (i, j >= 2) pairs from lists, the special
+// strategies wave-uniform, paid only for m > 5 (C5-shaped 446 -> 470, CBgems m7 +0.9 %; the m5 north
+// star -1.7 %). Round 5 put the special strategies on lists too (the s = 0 list holds only the
+// emitter / environment vertices), and the lists now win at m5 as well: north star 721.7 -> 730.4,
+// CBspheres 674 -> 684 Msamples/s, C5-shaped and CBgems m7 unchanged (profiles/r05za_ab_conn_lists.log).
 // Materials and lights copied to LDS (static arrays) when they fit: per-lane material / light
 // reads in the walk and in every connection become ds_reads instead of vector-memory loads.
 // (measured: C2 +3%, Lucy stand-in +1%, CBgems +1%)
@@ -291,16 +290,15 @@ struct ConnState {
 };
 
 // The connections of one pixel-sample (est_radiance_global_illumination's s x t loop,
-// bidirection.cpp:472-500): the wave enumerates the (i, j) strategies in uniform nested loops,
-// so the j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per iteration
-// for all lanes instead of interleaving with the general case; every connection that needs a
-// visibility ray is pushed (ballot + mbcnt compaction) into the wave's LDS ring, and whenever 64
-// are queued the wave traces them together. PA: the path accessor (PathsInRegs over the lane's
-// private Paths).
-template <int LM, bool EXT, bool COMPACT, bool STATS, class PA>
+// bidirection.cpp:472-500): one strategy kind at a time, each lane walking its own list of usable
+// vertices, so the j == 1 (fresh light sample) and i == 1 (camera connection) bodies run once per
+// iteration for all lanes instead of interleaving with the general case; every connection that
+// needs a visibility ray is pushed (ballot + mbcnt compaction) into the wave's LDS ring, and
+// whenever 64 are queued the wave traces them together. PA: the path accessor (PathsInRegs over the
+// lane's private Paths).
+template <int LM, bool EXT, bool STATS, class PA>
 __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, const PA& PP, Rng& g, int nE, int nL,
                                                int lane, float inv, ConnState& cs, Counters& cnt) {
-  const int wE = wave_max(nE), wL = wave_max(nL);
 #ifdef BDPT_PHASE_PROF
   const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
   unsigned long long tp0, tp1;
@@ -348,19 +346,36 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
 #endif
     }
   };
-  if constexpr (COMPACT) {
-  // The special strategies wave-uniformly: s = 0 (j = 0), the fresh light sample (j = 1),
-  // light tracing to the camera (i = 1, j >= 2) ...
-  for (int i = 2; i < wE; i++) conn_step(i, 0, i < nE);
-  for (int i = 1; i < wE; i++) conn_step(i, 1, i < nE && nL > 1);
-  for (int j = 2; j < wL; j++) conn_step(1, j, j < nL);
-  // ... then the general (i >= 2, j >= 2) pairs from per-lane lists of connectable vertices:
-  // a lane walks its own (i, j) pairs, so the wave iterates max(pairs) times instead of
-  // max|E| x max|L| (most cells of that grid are empty for most lanes)
-  using Mask = decltype(PP.dE);   // 32 bits, or 64 for the m <= 32 kernel
-  Mask mE = 0, mL = 0;
-  for (int k = 2; k < nE; k++) mE |= Mask(PP.e(k).cq > 0.0f ? 1u : 0u) << k;
+  // Per-lane lists (bit masks) of the vertices each strategy can use: connectable eye / light
+  // vertices (cq > 0), and the eye vertices an s = 0 path ends on (an emitter, or the environment
+  // in EXT kernels) — the only ones make_conn does not reject at once for these strategies
+  using Mask = decltype(PP.dE);   // 32 bits, or 64 for the m <= 32 / 62 kernels
+  Mask mE = 0, mL = 0, m0 = 0;
+  for (int k = 2; k < nE; k++) {
+    const Vtx v = PP.e(k);
+    mE |= Mask(v.cq > 0.0f ? 1u : 0u) << k;
+    const bool src = (EXT && is_env(v)) || (v.mat >= 0 && kp.S.mats[v.mat].type == MAT_EMISSION);
+    m0 |= Mask(src ? 1u : 0u) << k;
+  }
   for (int k = 2; k < nL; k++) mL |= Mask(PP.l(k).cq > 0.0f ? 1u : 0u) << k;
+  // The special strategies one kind at a time (each iteration runs one make_conn body for all
+  // lanes), every lane walking its own list in the reference's index order, so the wave iterates
+  // the longest list instead of the longest subpath: s = 0 (j = 0), the fresh light sample (j = 1:
+  // the camera, i = 1, and every connectable eye vertex), light tracing to the camera (i = 1, j >= 2)
+  auto each = [&](Mask m, int fixed, bool fixed_is_j) {
+    while (__ballot(m != 0)) {
+      const bool act = m != 0;
+      const int k = act ? ctz_mask(m) : 0;
+      conn_step(fixed_is_j ? k : fixed, fixed_is_j ? fixed : k, act);
+      if (act) m &= m - 1;
+    }
+  };
+  each(m0, 0, true);
+  each(nL > 1 ? Mask(mE | Mask(2u)) : Mask(0), 1, true);
+  each(mL, 1, false);
+  // ... then the general (i >= 2, j >= 2) pairs from the same lists: a lane walks its own (i, j)
+  // pairs, so the wave iterates max(pairs) times instead of max|E| x max|L| (most cells of that
+  // grid are empty for most lanes)
   if (mL == 0) mE = 0;
   Mask jm = mL;
   while (__ballot(mE != 0)) {
@@ -371,10 +386,6 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
       jm &= jm - 1;
       if (jm == 0) { mE &= mE - 1; jm = mL; }
     }
-  }
-  } else {
-  for (int i = 1; i < wE; i++)
-    for (int j = 0; j < wL; j++) conn_step(i, j, i < nE && j < nL);
   }
 #ifdef BDPT_PHASE_PROF
   cs.ph_gen += __builtin_amdgcn_s_memtime() - tg0;
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
       ph_cells += (unsigned)(max(wave_max(nE) - 1, 0) * wave_max(nL));
       ph_pairs += (unsigned)(max(nE - 1, 0) * nL);
 #endif
-      connect_sample<LM, EXT, conn_compact<MAXV>(), STATS>(kp, q, PathsInRegs<MAXV, EXT>(P), g, nE, nL, lane, inv, cs, cnt);
+      connect_sample<LM, EXT, STATS>(kp, q, PathsInRegs<MAXV, EXT>(P), g, nE, nL, lane, inv, cs, cnt);
     }
     finish_item<LM>(kp, q, it, lane, cs, cnt);
 #ifdef BDPT_PHASE_PROF
