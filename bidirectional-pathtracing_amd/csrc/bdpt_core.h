@@ -1409,6 +1409,8 @@ struct Paths {
   VtxS L[MAXV + 1];   // L[k] at index k-1 (k >= 1): L[1] = light vertex, then hits
   int nE, nL;        // path sizes including v0, v1 (reference's vector sizes)
   DeltaMask<MAXV> dE, dL;   // delta-BSDF bit masks: bit k set <=> E[k] / L[k] is_delta()
+  DeltaMask<MAXV> cE, cL;   // connectable vertices: bit k set <=> E[k] / L[k] has cq > 0
+  DeltaMask<MAXV> sE;       // s = 0 sources: bit k set <=> E[k] is on an emitter or the environment
   float l1_dir_pdf;
   f3 l1_d;           // the light walk's first direction and its pdf (read back when it starts)
   float l1_pdf;
@@ -1648,6 +1650,9 @@ struct PathsInRegs {
   const Paths<MAXV>& P;
   DeltaMask<MAXV> dE, dL;
   BDPT_HD explicit PathsInRegs(const Paths<MAXV>& p) : P(p), dE(p.dE), dL(p.dL) {}
+  BDPT_HD DeltaMask<MAXV> conn_e() const { return P.cE; }   // connectable eye / light vertices
+  BDPT_HD DeltaMask<MAXV> conn_l() const { return P.cL; }
+  BDPT_HD DeltaMask<MAXV> src_e() const { return P.sE; }    // s = 0 sources
   BDPT_HD Vtx e(int k) const { return vtx_load<EXT>(P.E[k - 2]); }
   BDPT_HD Vtx l(int k) const { return vtx_load<EXT>(P.L[k - 1]); }
 };
@@ -1664,6 +1669,7 @@ struct WalkState {
   float pv_fwd, pv_gp, pv_q;   // the previous vertex's fwd / prefix / roulette probability
   int i, count, pv_mat;        // reference vertex index, vertices stored on this subpath, previous material
   DeltaMask<MAXV> dm;          // delta mask of this subpath
+  DeltaMask<MAXV> cm, em;      // its connectable vertices (cq > 0); the eye subpath's s = 0 sources
   uint32_t lpos;               // the light stream's position after L[1]
   bool light, l1env;           // walking the light subpath; its L[1] is an environment vertex
 };
@@ -1783,6 +1789,8 @@ BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>&
   w.i = 2;
   w.count = 0;
   w.dm = 0;
+  w.cm = 0;
+  w.em = 0;
   w.light = false;
   w.pv_mat = -1;
   w.pv_fwd = 1.0f; w.pv_gp = 0.0f; w.pv_q = 1.0f;
@@ -1796,7 +1804,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
   f3 ro = w.ro, rd = w.rd, prev_n = w.prev_n, nalpha = w.nalpha;
   float rmin = w.rmin, rmax = w.rmax, pv_fwd = w.pv_fwd, pv_gp = w.pv_gp, pv_q = w.pv_q;
   int i = w.i, count = w.count, pv_mat = w.pv_mat;
-  DeltaMask<MAXV> dm = w.dm;
+  DeltaMask<MAXV> dm = w.dm, cm = w.cm, em = w.em;
   bool light = w.light, l1env = w.l1env;
   auto next_alpha = walk_next_alpha;
   bool done = false;
@@ -1828,6 +1836,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
         v.fwd = pdf_b(S.mats[pm], pn, pn, rd) * pv_q * 1.0f;
       }
       v.gp = 0.0f;
+      em |= DeltaMask<MAXV>(1) << i;   // an s = 0 source (vertex index i = count + 2)
       vtx_store<EXT>(P.E[count++], v);
     }
     if (!end) {
@@ -1847,6 +1856,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       v.fwd = 1; v.gp = EXT ? 1.0f : 0.0f; v.cq = 0;
       VtxS* slot = (light ? P.L + 1 : P.E) + count++;
       if (is_delta(M.type)) dm |= DeltaMask<MAXV>(1) << i;
+      if (!light && M.type == MAT_EMISSION) em |= DeltaMask<MAXV>(1) << i;   // an s = 0 source
       // eye_constants / light_constants of this vertex at its creation. The previous vertex is the
       // one just below it on the same subpath (camera: no step; the light vertex L[1] for the
       // light's first hit) and is still in registers: position ro, normal prev_n (shading axis
@@ -1889,6 +1899,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       const bool gp_t = !((dm >> (i - 2)) & 3u);
       auto finish = [&](float q) {   // q: this vertex's roulette probability (1 without roulette)
         v.cq = conn ? (EXT ? q : 1.0f) : 0.0f;
+        if (v.cq > 0.0f) cm |= DeltaMask<MAXV>(1) << i;   // connectable (i: this vertex's index)
         v.gp = first_eye ? 0.0f : mis_horner(((EXT ? gp_pp * q : gp_pp) * gp_g) / pfwd, gp_t, pgp);
         pv_mat = v.mat; pv_fwd = v.fwd; pv_gp = v.gp; pv_q = q;
       };
@@ -1939,10 +1950,13 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       if (light) {
         P.nL = count + 2;
         P.dL = dm;
+        P.cL = cm;
         done = true;
       } else {
       P.nE = count + 2;
       P.dE = dm;
+      P.cE = cm;
+      P.sE = em;
       light = true;
       // the light sample drawn before the eye walk, read back from the path store (not held in
       // registers across the eye walk)
@@ -1953,14 +1967,14 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       const float mis_p = P.L[0].fwd;
       l1env = vs_mat(P.L[0]) == (int)MAT_ENV_V;
       rmin = BDPT_EPS_F; rmax = INFINITY;
-      i = 2; count = 0; dm = 0;
+      i = 2; count = 0; dm = 0; cm = 0;
       pv_mat = -1; pv_fwd = mis_p; pv_gp = 0.0f; pv_q = 1.0f;   // the light vertex L[1]
       }
     }
   }
   w.ro = ro; w.rd = rd; w.prev_n = prev_n; w.nalpha = nalpha;
   w.rmin = rmin; w.rmax = rmax; w.pv_fwd = pv_fwd; w.pv_gp = pv_gp; w.pv_q = pv_q;
-  w.i = i; w.count = count; w.pv_mat = pv_mat; w.dm = dm; w.light = light; w.l1env = l1env;
+  w.i = i; w.count = count; w.pv_mat = pv_mat; w.dm = dm; w.cm = cm; w.em = em; w.light = light; w.l1env = l1env;
   return done;
 }
 

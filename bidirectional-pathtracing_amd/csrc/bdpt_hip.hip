@@ -346,18 +346,14 @@ __device__ __forceinline__ void connect_sample(const KParams& kp, WaveQ& q, cons
 #endif
     }
   };
-  // Per-lane lists (bit masks) of the vertices each strategy can use: connectable eye / light
-  // vertices (cq > 0), and the eye vertices an s = 0 path ends on (an emitter, or the environment
-  // in EXT kernels) — the only ones make_conn does not reject at once for these strategies
+  // Per-lane lists (bit masks, built by the walk as it stores the vertices) of the vertices each
+  // strategy can use: connectable eye / light vertices (cq > 0), and the eye vertices an s = 0 path
+  // ends on (an emitter, or the environment in EXT kernels) — the only ones make_conn does not
+  // reject at once for these strategies
   using Mask = decltype(PP.dE);   // 32 bits, or 64 for the m <= 32 / 62 kernels
-  Mask mE = 0, mL = 0, m0 = 0;
-  for (int k = 2; k < nE; k++) {
-    const Vtx v = PP.e(k);
-    mE |= Mask(v.cq > 0.0f ? 1u : 0u) << k;
-    const bool src = (EXT && is_env(v)) || (v.mat >= 0 && kp.S.mats[v.mat].type == MAT_EMISSION);
-    m0 |= Mask(src ? 1u : 0u) << k;
-  }
-  for (int k = 2; k < nL; k++) mL |= Mask(PP.l(k).cq > 0.0f ? 1u : 0u) << k;
+  // (a lane without a sample in this step, nE = 0, still holds its previous sample's paths)
+  const bool has = nE > 0;
+  Mask mE = has ? PP.conn_e() : Mask(0), mL = has ? PP.conn_l() : Mask(0), m0 = has ? PP.src_e() : Mask(0);
   // The special strategies one kind at a time (each iteration runs one make_conn body for all
   // lanes), every lane walking its own list in the reference's index order, so the wave iterates
   // the longest list instead of the longest subpath: s = 0 (j = 0), the fresh light sample (j = 1:
