@@ -12,15 +12,21 @@ pixel (265.4 M pixel-samples) through the C-ABI (libbdpt_amd.so, k_bdpt_sample).
 Other BASELINE configs: --workload c2 | c3 | c4 | c5 (c5's ennis.exr is an LFS pointer in the
 reference: a synthetic sky of the same role stands in, tools/envmap.py).
 
-Multi-GPU (torchrun, one rank per GPU), strong scaling by default: the step's fixed render (the
-workload's spp of every pixel) is split by sample range — rank r renders global sample indices
-[s*spp + r*spp/N, s*spp + (r+1)*spp/N) of step s (sample keys are global, so the image does not
-depend on N up to fp32 summation order) — and the W*H*3 fp32 frames are summed by one all-reduce
-inside the timed region (splats land anywhere, so a tile gather would not do). The
-split and the reduce are the product's bdpt_amd.ShardedRender; --dist-backend picks RCCL ("nccl",
-the default) or gloo (the same all_reduce of the device tensor; two ranks can then share one GPU,
---devices 0,0, as tests/test_gpu_multirank.py runs it). --scaling weak gives every rank the full
-spp instead. value = pixel-samples of all ranks / max-over-ranks wall time.
+Multi-GPU, strong scaling by default: the step's fixed render (the workload's spp of every pixel)
+is split by sample range — rank r renders global sample indices [s*spp + r*spp/N,
+s*spp + (r+1)*spp/N) of step s (sample keys are global, so the image does not depend on N up to
+fp32 summation order) — and the W*H*3 fp32 frames are summed inside the timed region (splats land
+anywhere, so a tile gather would not do). Two launch forms (plan_launch):
+* `python bench.py --gpus N` (no launcher): N contexts in this process on devices 0..N-1 (or
+  --devices), rendered concurrently, summed by the C-ABI's RCCL reduce (bdpt_reduce_frames, the
+  CLI's -g N) into context 0's frames; `rccl_ranks` = the communicator's ranks (distinct devices);
+* under torchrun (WORLD_SIZE set, must equal --gpus): one rank per GPU, bdpt_amd.ShardedRender's
+  all-reduce of the sample frame; --dist-backend picks RCCL ("nccl", the default) or gloo (the
+  same all_reduce of the device tensor; two ranks can then share one GPU, --devices 0,0, as
+  tests/test_gpu_multirank.py runs it).
+--scaling weak gives every rank the full spp instead. value = pixel-samples of all ranks /
+max-over-ranks wall time. A named workload refuses to run with a product knob set in the
+environment (PRODUCT_KNOBS); every BDPT_* variable is recorded in config.env.
 """
 from __future__ import annotations
 
@@ -271,92 +277,94 @@ def load_traffic(workload: str, kernel_ms: float):
     return b, info
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="ns",
-                    help="ns = the north-star target (default); c2..c5 = BASELINE.json configs[1..4]")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                    help="strong: the workload's fixed render split across ranks (default); "
-                         "weak: every rank renders the full spp")
-    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
-                    help="torch.distributed backend for N>1: nccl (= RCCL on ROCm, the default) or gloo "
-                         "(same all_reduce of the device frame; lets two ranks share one GPU in tests)")
-    ap.add_argument("--devices", default=None,
-                    help="device of each rank, comma-separated (default: LOCAL_RANK), e.g. 0,0")
-    ap.add_argument("--dump-frame", default=None,
-                    help="rank 0 saves the last step's reduced sample frame (.npy, H x W x 3)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--scene", default=None, help="override: a .dae path")
-    ap.add_argument("--width", type=int, default=None)
-    ap.add_argument("--height", type=int, default=None)
-    ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--max-depth", type=int, default=None)
-    ap.add_argument("--pipeline", type=int, choices=[0, 1], default=0, help="0 auto = 1 megakernel")
-    ap.add_argument("--envmap", default=None,
-                    help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
-                         "synthetic sky of tools/envmap.py (the reference's exr/*.exr are LFS pointers)")
-    ap.add_argument("--rr", action="store_true", help="Russian roulette on both subpaths")
-    ap.add_argument("--integrator", choices=["bdpt", "pt"], default="bdpt",
-                    help="bdpt (the reference's BidirectionalPathTracer, the headline) or pt (its "
-                         "unidirectional PathTracer, DESIGN.md §10; adaptive sampling off: every "
-                         "pixel takes all spp; ranks split the frame into row bands)")
-    args = ap.parse_args()
-    wl = WORKLOADS[args.workload]
-    scene_path = args.scene or os.path.join(REPO, wl[0])
-    W = args.width or wl[1]
-    H = args.height or wl[2]
-    SPP = args.spp or wl[3]
-    M = args.max_depth if args.max_depth is not None else wl[4]
-    envmap = args.envmap if args.envmap is not None else wl[5]
-    rr = args.rr or wl[6]
-    named = (args.scene is None and args.width is None and args.height is None and args.spp is None
-             and args.max_depth is None and args.envmap is None and not args.rr)
-    ensure_standin(scene_path)
+# Run-time switches of the product library that change its tree or its kernel (bdpt_hip.hip
+# bdpt_create, bdpt_scene.cpp build_host_scene): a named (headline) workload refuses to run with any
+# of them set, so the line always states the product configuration; every BDPT_* variable that is
+# set goes into config.env.
+PRODUCT_KNOBS = ("BDPT_LDS_MODE", "BDPT_NTOP_MAX", "BDPT_BLOCK_MAJOR", "BDPT_XCD_GROUPS",
+                 "BDPT_BVH", "BDPT_SAH_LEAF", "BDPT_SAH_CT", "BDPT_SAH_BINS")
 
+
+def knob_env(environ) -> dict:
+    """every BDPT_* variable of the environment (recorded in config.env)"""
+    return {k: environ[k] for k in sorted(environ) if k.startswith("BDPT_")}
+
+
+def check_knobs(environ, named: bool) -> None:
+    """A named workload is the product configuration: refuse if a product knob is set."""
+    bad = [k for k in PRODUCT_KNOBS if k in environ]
+    if named and bad:
+        raise SystemExit(f"bench.py: {', '.join(f'{k}={environ[k]}' for k in bad)} set: these change the "
+                         f"product's tree / kernel, so a named workload (the headline) refuses to run; unset "
+                         f"them, or give an explicit --scene / --width / ... configuration to measure a variant")
+
+
+def plan_launch(gpus: int, world_size_env, devices_arg, ndev: int) -> dict:
+    """How `bench.py --gpus N` runs, decided before anything touches a GPU:
+    * "torchrun": WORLD_SIZE is set (one process per GPU under torch.distributed.run); it must
+      equal --gpus;
+    * "single": no WORLD_SIZE and --gpus 1: one context;
+    * "inprocess": no WORLD_SIZE and --gpus N > 1: N contexts in this process on devices
+      0..N-1 (or --devices), their sample ranges rendered concurrently and the frames summed by
+      the C-ABI's RCCL reduce (bdpt_reduce_frames) inside the timed region.
+    Raises SystemExit (non-zero) on a mismatch: too few visible devices, a --devices list of the
+    wrong length, or WORLD_SIZE != --gpus."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} < 1")
+    devmap = [int(x) for x in devices_arg.split(",")] if devices_arg else None
+    if devmap is not None and any(d < 0 for d in devmap):
+        raise SystemExit(f"bench.py: negative device in --devices {devices_arg}")
+    if world_size_env is not None:
+        world = int(world_size_env)
+        if world != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} (torchrun) but --gpus {gpus}: they must agree")
+        return {"mode": "torchrun", "world": world, "devmap": devmap}
+    if devmap is not None and len(devmap) != gpus:
+        raise SystemExit(f"bench.py: --devices lists {len(devmap)} devices for --gpus {gpus}")
+    devices = devmap or list(range(gpus))
+    if max(devices) >= ndev:
+        raise SystemExit(f"bench.py: --gpus {gpus} needs device {max(devices)}, but only {ndev} visible")
+    return {"mode": "single" if gpus == 1 else "inprocess", "world": gpus, "devices": devices}
+
+
+class Timed:
+    """what a timed region measured: wall seconds (max over ranks), rank 0's mean launch ms, and
+    per-rank rows (elapsed s, kernel ms, pixel-samples per step, device)"""
+
+    def __init__(self, elapsed, kern_ms, rows, world):
+        self.elapsed, self.kern_ms, self.rows, self.world = elapsed, kern_ms, rows, world
+
+    @property
+    def samples_per_step(self) -> float:
+        return sum(r[2] for r in self.rows)
+
+
+def run_torchrun_or_single(args, B, scene, W, H, SPP, M, rr, seed, plan, use_pt, scaling):
+    """One context per process: the plain N=1 path (no WORLD_SIZE) or one rank under torchrun
+    (bdpt_amd.ShardedRender: this rank's sample range, bdpt_copy_frame, one all-reduce)."""
     import numpy as np
     import torch
-    import bdpt_amd as B
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = plan["world"]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    devmap = [int(x) for x in args.devices.split(",")] if args.devices else None
-    gpu = devmap[rank % len(devmap)] if devmap else (local if world > 1 else 0)
+    if plan["mode"] == "torchrun":
+        devmap = plan["devmap"]
+        gpu = devmap[rank % len(devmap)] if devmap else local
+    else:
+        gpu = plan["devices"][0]
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
     # under torchrun (WORLD_SIZE set) the process group is made at every world size, 1 included, so
     # the RCCL all-reduce of the frame runs on one GPU exactly as it does on eight
-    if world > 1 or "WORLD_SIZE" in os.environ:
+    if plan["mode"] == "torchrun":
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-
-    t_load = time.perf_counter()
-    scene = B.load_dae(scene_path, W, H)      # bdpt_dae_load: the CLI's scene path
-    t_load = time.perf_counter() - t_load
-    env_desc = None
-    if envmap:
-        if envmap.startswith("synth:"):
-            sys.path.insert(0, os.path.join(REPO, "tools"))
-            from envmap import synth_envmap
-            ew, eh = (int(v) for v in envmap[6:].split("x"))
-            scene.set_envmap(synth_envmap(ew, eh))
-            env_desc = f"synthetic sky {ew}x{eh} (tools/envmap.py)"
-        else:
-            scene.set_envmap(B.load_exr(envmap))
-            env_desc = os.path.basename(envmap)
-    seed = 5489
     stream = torch.cuda.Stream(dev)          # a real stream: handle 0 would mean "ctx's own"
     torch.cuda.set_stream(stream)
-    use_pt = args.integrator == "pt"
-    scaling = "strong" if use_pt else args.scaling
     band = [(0, H * rank // world, W, H * (rank + 1) // world - H * rank // world)]
     t_create = time.perf_counter()
     if use_pt:   # whole pixels: each rank renders its row band with all SPP samples
@@ -402,16 +410,186 @@ def main() -> int:
     rank_samples = int(pt.read_sample_counts().astype(np.int64)[band[0][1]:band[0][1] + band[0][3]].sum()) \
         if use_pt else W * H * sh.samples(0)
     rows = sh.gather_floats([elapsed, kern_ms, float(rank_samples), float(gpu)])
-    rank_elapsed = [r[0] for r in rows]
-    rank_kern = [r[1] for r in rows]
-    elapsed = max(rank_elapsed)
-    samples_per_step = sum(r[2] for r in rows)
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, frame.cpu().numpy().reshape(H, W, 3))
     pt.close()
+    t = Timed(max(r[0] for r in rows), kern_ms, rows, world)
+    t.rank, t.dist, t.dev, t.t_create = rank, dist, dev, t_create
+    t.rccl_ranks = None
+    t.label = ("" if dist is None else " + RCCL all-reduce" if args.dist_backend == "nccl" else " + gloo all-reduce")
+    t.backend = args.dist_backend if dist is not None else None
+    return t
 
-    # algorithmic bytes of this rank's launch: in-kernel counters on a separate, untimed launch of
+
+def run_inprocess(args, B, scene, W, H, SPP, M, rr, seed, plan, use_pt, scaling):
+    """N contexts in this one process (no launcher), one per device of plan["devices"] (the
+    CLI's -g N form, pathtracer_cli.cpp): per step every context clears its frames and renders its
+    sample range (or, for the PathTracer, its row band) on a stream of its device — the launches
+    are asynchronous, so the devices render concurrently — then ONE bdpt_reduce_frames (RCCL
+    ncclReduce over the distinct devices; contexts sharing a device are summed on it first) puts the
+    whole frame into context 0's. The clear keeps every step's reduced frame equal to one render
+    of that step's samples. Reference: raytraced_renderer.cpp:323-327 (the N worker threads this
+    replaces), bidirection.cpp:457-466 (why a whole-frame sum)."""
+    import numpy as np
+    import torch
+    devices = plan["devices"]
+    N = len(devices)
+    torch.cuda.set_device(devices[0])
+    streams = [torch.cuda.Stream(torch.device("cuda", d)) for d in devices]
+    t_create = time.perf_counter()
+    pts = []
+    for r, d in enumerate(devices):
+        if use_pt:
+            p = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=d, max_tolerance=0.0)
+        else:
+            p = B.BidirectionalPathTracer(scene, W, H, SPP if scaling == "strong" else SPP * N, M, seed=seed,
+                                          device=d, pipeline=args.pipeline, russian_roulette=rr)
+        p.set_stream(streams[r].cuda_stream)
+        pts.append(p)
+    red = B.FrameReducer(pts)
+    t_create = time.perf_counter() - t_create
+    bands = [(0, H * r // N, W, H * (r + 1) // N - H * r // N) for r in range(N)]
+
+    def sync_all():
+        for d in devices:
+            torch.cuda.synchronize(d)
+
+    evs = []
+
+    def step(k: int, timed: bool):
+        for r, p in enumerate(pts):
+            p.clear()
+            if timed:
+                with torch.cuda.device(devices[r]):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(streams[r])
+            if use_pt:
+                p.raytrace_tiles([bands[r]], 0, SPP)
+            else:
+                base, n = B.rank_sample_range(k, r, N, SPP, scaling)
+                if n > 0:
+                    p.raytrace_tiles([], base, n)
+            if timed:
+                with torch.cuda.device(devices[r]):
+                    e1.record(streams[r])
+                evs.append((r, e0, e1))
+        red.reduce(0)                               # RCCL: every device's frames into context 0's
+
+    for k in range(args.warmup):
+        step(k, False)
+    sync_all()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, True)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    kms = [float(np.mean([a.elapsed_time(b) for r_, a, b in evs if r_ == r])) for r in range(N)]
+    if use_pt:
+        samples = [int(p.read_sample_counts().astype(np.int64)[b[1]:b[1] + b[3]].sum()) for p, b in zip(pts, bands)]
+        # context 0 holds the reduced counts: its own band is its own samples (the others' bands
+        # were zero in it before the reduce and are summed in after)
+    else:
+        samples = [W * H * B.rank_sample_range(0, r, N, SPP, scaling)[1] for r in range(N)]
+    if args.dump_frame:
+        np.save(args.dump_frame, pts[0].read_frame(B.FRAME_SAMPLE))
+    rccl_ranks = red.ranks
+    red.close()
+    for p in pts:
+        p.close()
+    rows = [[elapsed, kms[r], float(samples[r]), float(devices[r])] for r in range(N)]
+    t = Timed(elapsed, kms[0], rows, N)
+    t.rank, t.dist, t.dev, t.t_create = 0, None, torch.device("cuda", devices[0]), t_create
+    t.rccl_ranks = rccl_ranks
+    t.label = f" + RCCL reduce (bdpt_reduce_frames: {N} contexts in one process, {rccl_ranks} RCCL rank(s))"
+    t.backend = "rccl (bdpt_reduce_frames, one process)"
+    return t
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs: under torchrun it must equal WORLD_SIZE; without a launcher, N > 1 runs N "
+                         "contexts in this process (devices 0..N-1 or --devices) with the RCCL frame reduce")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="ns",
+                    help="ns = the north-star target (default); c2..c5 = BASELINE.json configs[1..4]")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: the workload's fixed render split across ranks (default); "
+                         "weak: every rank renders the full spp")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend under torchrun: nccl (= RCCL on ROCm, the default) or "
+                         "gloo (same all_reduce of the device frame; lets two ranks share one GPU in tests)")
+    ap.add_argument("--devices", default=None,
+                    help="device of each rank / context, comma-separated (default: LOCAL_RANK under "
+                         "torchrun, 0..N-1 in one process), e.g. 0,0")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the last step's reduced sample frame (.npy, H x W x 3)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--scene", default=None, help="override: a .dae path")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--max-depth", type=int, default=None)
+    ap.add_argument("--pipeline", type=int, choices=[0, 1], default=0, help="0 auto = 1 megakernel")
+    ap.add_argument("--envmap", default=None,
+                    help="environment light (DESIGN.md §9): an .exr path, or synth:WxH for the "
+                         "synthetic sky of tools/envmap.py (the reference's exr/*.exr are LFS pointers)")
+    ap.add_argument("--rr", action="store_true", help="Russian roulette on both subpaths")
+    ap.add_argument("--integrator", choices=["bdpt", "pt"], default="bdpt",
+                    help="bdpt (the reference's BidirectionalPathTracer, the headline) or pt (its "
+                         "unidirectional PathTracer, DESIGN.md §10; adaptive sampling off: every "
+                         "pixel takes all spp; ranks split the frame into row bands)")
+    args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    scene_path = args.scene or os.path.join(REPO, wl[0])
+    W = args.width or wl[1]
+    H = args.height or wl[2]
+    SPP = args.spp or wl[3]
+    M = args.max_depth if args.max_depth is not None else wl[4]
+    envmap = args.envmap if args.envmap is not None else wl[5]
+    rr = args.rr or wl[6]
+    named = (args.scene is None and args.width is None and args.height is None and args.spp is None
+             and args.max_depth is None and args.envmap is None and not args.rr)
+    check_knobs(os.environ, named)
+    knobs = knob_env(os.environ)
+
+    import numpy as np
+    import torch
+    import bdpt_amd as B
+
+    # decided before any GPU call (device_count does not initialise HIP on this image)
+    plan = plan_launch(args.gpus, os.environ.get("WORLD_SIZE"), args.devices,
+                       0 if "WORLD_SIZE" in os.environ else torch.cuda.device_count())
+    ensure_standin(scene_path)
+
+    t_load = time.perf_counter()
+    scene = B.load_dae(scene_path, W, H)      # bdpt_dae_load: the CLI's scene path
+    t_load = time.perf_counter() - t_load
+    env_desc = None
+    if envmap:
+        if envmap.startswith("synth:"):
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from envmap import synth_envmap
+            ew, eh = (int(v) for v in envmap[6:].split("x"))
+            scene.set_envmap(synth_envmap(ew, eh))
+            env_desc = f"synthetic sky {ew}x{eh} (tools/envmap.py)"
+        else:
+            scene.set_envmap(B.load_exr(envmap))
+            env_desc = os.path.basename(envmap)
+    seed = 5489
+    use_pt = args.integrator == "pt"
+    scaling = "strong" if use_pt else args.scaling
+    run = run_inprocess if plan["mode"] == "inprocess" else run_torchrun_or_single
+    t = run(args, B, scene, W, H, SPP, M, rr, seed, plan, use_pt, scaling)
+    world, rank, dist, dev, rows = t.world, t.rank, t.dist, t.dev, t.rows
+    kern_ms, elapsed = t.kern_ms, t.elapsed
+    samples_per_step = t.samples_per_step
+
+    # algorithmic bytes of rank 0's launch: in-kernel counters on a separate, untimed launch of
     # the same work (counting perturbs timing), SURVEY.md §8d.
+    band = [(0, H * rank // world, W, H * (rank + 1) // world - H * rank // world)]
     if use_pt:
         ps = B.PathTracer(scene, W, H, SPP, M, seed=seed, device=dev.index, max_tolerance=0.0,
                           collect_stats=True)
@@ -458,14 +636,15 @@ def main() -> int:
                    + (" unidirectional PathTracer" if use_pt else "")
                    + (", whole frame per step split across GPUs" if scaling == "strong" else ", full spp per GPU")
                    + (" (row bands)" if use_pt else " (sample ranges)")
-                   + ("" if dist is None else " + RCCL all-reduce" if args.dist_backend == "nccl"
-                      else " + gloo all-reduce"),
+                   + t.label,
                    "workload_key": args.workload if named else "custom",
                    "pipeline": ["auto (megakernel)", "megakernel"][args.pipeline],
                    "scene": os.path.relpath(scene_path, REPO), "width": W, "height": H, "spp": SPP,
                    "max_depth": M, "envmap": env_desc, "russian_roulette": rr,
                    "parallelism": f"{'row bands' if use_pt else 'sample ranges'} x{world}",
-                   "host_setup_s": {"dae_load": round(t_load, 3), "bdpt_create": round(t_create, 3)}},
+                   "launch": plan["mode"],
+                   "env": knobs,
+                   "host_setup_s": {"dae_load": round(t_load, 3), "bdpt_create": round(t.t_create, 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                      "traffic": traffic, "kernel": "k_pt" if use_pt else "k_bdpt_sample",
@@ -498,11 +677,13 @@ def main() -> int:
     }
     if traffic_info:
         out["roofline"]["traffic_pmc"] = traffic_info
-    if dist is not None:
-        out["per_rank"] = {"elapsed_s": [round(x, 4) for x in rank_elapsed],
-                           "kernel_ms": [round(x, 3) for x in rank_kern],
+    if t.rccl_ranks is not None:
+        out["rccl_ranks"] = t.rccl_ranks
+    if world > 1 or dist is not None:
+        out["per_rank"] = {"elapsed_s": [round(r[0], 4) for r in rows],
+                           "kernel_ms": [round(r[1], 3) for r in rows],
                            "samples_per_step": [int(r[2]) for r in rows], "device": [int(r[3]) for r in rows],
-                           "backend": args.dist_backend}
+                           "backend": t.backend}
     if use_pt:
         out["config"]["integrator"] = "PathTracer (pathtracer.cpp:47-340)"
     cores = host_cores()

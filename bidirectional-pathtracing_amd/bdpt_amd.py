@@ -382,11 +382,14 @@ class BidirectionalPathTracer:
             p.direct_hemisphere_sample = 1 if _pt["direct_hemisphere_sample"] else 0
             p.lens_radius, p.focal_distance = _pt["lens_radius"], _pt["focal_distance"]
         self._desc = scene.desc()
+        self._reducers = []   # FrameReducers over this context: closed before it is destroyed
         ctx = C.c_void_p()
         _check(self.lib.bdpt_create(C.byref(self._desc), C.byref(p), C.byref(ctx)), self.lib)
         self.ctx = ctx
 
     def close(self) -> None:
+        for red in list(getattr(self, "_reducers", ())):
+            red.close()
         if getattr(self, "ctx", None):
             self.lib.bdpt_destroy(self.ctx)
             self.ctx = None
@@ -483,15 +486,20 @@ class FrameReducer:
     the CLI's -g N: one RCCL communicator clique over their distinct devices (contexts sharing a
     device are summed on it first), and per reduce(root) one grouped ncclReduce of every
     renderer's eye and light frames into the root renderer's. Afterwards root.read_frame() is the
-    whole image; the others' frames are unchanged."""
+    whole image; the others' frames are unchanged. Closing any of its renderers closes the reducer
+    first (bdpt_reduce_destroy then touches no context)."""
 
     def __init__(self, renderers: Sequence["BidirectionalPathTracer"]):
         self.lib = load_library()
-        self.renderers = list(renderers)   # the contexts must outlive the reducer
+        self.renderers = list(renderers)
+        if any(not getattr(r, "ctx", None) for r in self.renderers):
+            raise BDPTError("FrameReducer: a renderer is closed")
         arr = (C.c_void_p * len(self.renderers))(*[r.ctx.value for r in self.renderers])
         h = C.c_void_p()
         _check(self.lib.bdpt_reduce_create(arr, len(self.renderers), C.byref(h)), self.lib)
         self.h = h
+        for r in self.renderers:   # a renderer's close() closes its reducers first
+            r._reducers.append(self)
 
     @property
     def ranks(self) -> int:
@@ -499,12 +507,17 @@ class FrameReducer:
         return int(self.lib.bdpt_reduce_ranks(self.h))
 
     def reduce(self, root: int = 0) -> None:
+        if not getattr(self, "h", None):
+            raise BDPTError("FrameReducer is closed")
         _check(self.lib.bdpt_reduce_frames(self.h, root), self.lib)
 
     def close(self) -> None:
         if getattr(self, "h", None):
             self.lib.bdpt_reduce_destroy(self.h)
             self.h = None
+        for r in getattr(self, "renderers", ()):
+            if self in getattr(r, "_reducers", ()):
+                r._reducers.remove(self)
 
     def __del__(self):
         try:

@@ -117,6 +117,8 @@ struct bdpt_reducer {
   // rank -> scratch (eye | light | counts) for devices holding more than one ctx
   std::vector<float*> scratch;
   std::vector<hipEvent_t> ev;               // ctx index -> ordering event
+  std::vector<int> ctx_dev;                 // ctx index -> device (the reducer's own copy)
+  std::vector<hipEvent_t> done;             // rank -> recorded after its last reduce on its lead stream
   size_t npix = 0;
   bool pt = false;
 };
@@ -129,8 +131,11 @@ void free_reducer(bdpt_reducer* r) {
     if (r->comms[k]) (void)rccl().CommDestroy(r->comms[k]);
   for (size_t k = 0; k < r->scratch.size(); k++)
     if (r->scratch[k]) { (void)hipSetDevice(r->devs[k]); (void)hipFree(r->scratch[k]); }
+  // only the reducer's own data from here on: the contexts may already be destroyed
   for (size_t k = 0; k < r->ev.size(); k++)
-    if (r->ev[k]) { (void)hipSetDevice(r->ctxs[k]->device); (void)hipEventDestroy(r->ev[k]); }
+    if (r->ev[k]) { (void)hipSetDevice(r->ctx_dev[k]); (void)hipEventDestroy(r->ev[k]); }
+  for (size_t k = 0; k < r->done.size(); k++)
+    if (r->done[k]) { (void)hipSetDevice(r->devs[k]); (void)hipEventDestroy(r->done[k]); }
   delete r;
 }
 
@@ -145,12 +150,19 @@ int bdpt_reduce_create(void* const* ctxs, int32_t n, bdpt_reducer** out) {
   *out = nullptr;
   std::unique_ptr<bdpt_reducer, void (*)(bdpt_reducer*)> r(new bdpt_reducer(), free_reducer);
   for (int i = 0; i < n; i++) {
+    if (!ctxs[i]) { g_err = "bdpt_reduce_create: null ctx"; return BDPT_E_INVALID; }
+    for (int j = 0; j < i; j++)
+      if (ctxs[j] == ctxs[i]) { g_err = "bdpt_reduce_create: a ctx is listed twice"; return BDPT_E_INVALID; }
+  }
+  // every ctx is locked while its fields are read (address order, as bdpt_reduce_frames: a render
+  // or clear on another thread waits)
+  std::vector<Ctx*> order;
+  for (int i = 0; i < n; i++) order.push_back((Ctx*)ctxs[i]);
+  std::sort(order.begin(), order.end());
+  std::vector<std::unique_lock<std::recursive_mutex>> locks;
+  for (Ctx* c : order) locks.emplace_back(c->mu);
+  for (int i = 0; i < n; i++) {
     Ctx* c = (Ctx*)ctxs[i];
-    if (!c) { g_err = "bdpt_reduce_create: null ctx"; return BDPT_E_INVALID; }
-    if (std::find(r->ctxs.begin(), r->ctxs.end(), c) != r->ctxs.end()) {
-      g_err = "bdpt_reduce_create: a ctx is listed twice";
-      return BDPT_E_INVALID;
-    }
     if (i > 0 && (c->prm.width != r->ctxs[0]->prm.width || c->prm.height != r->ctxs[0]->prm.height ||
                   c->pt != r->pt)) {
       g_err = "bdpt_reduce_create: every ctx must have the same frame size and integrator";
@@ -158,6 +170,7 @@ int bdpt_reduce_create(void* const* ctxs, int32_t n, bdpt_reducer** out) {
     }
     if (i == 0) { r->npix = c->npix; r->pt = c->pt; }
     r->ctxs.push_back(c);
+    r->ctx_dev.push_back(c->device);
     auto it = std::find(r->devs.begin(), r->devs.end(), c->device);
     if (it == r->devs.end()) {
       r->devs.push_back(c->device);
@@ -184,6 +197,11 @@ int bdpt_reduce_create(void* const* ctxs, int32_t n, bdpt_reducer** out) {
   for (int i = 0; i < n; i++) {
     HIPCHK(hipSetDevice(r->ctxs[i]->device));
     HIPCHK(hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming));
+  }
+  r->done.assign(nr, nullptr);
+  for (int k = 0; k < nr; k++) {
+    HIPCHK(hipSetDevice(r->devs[k]));
+    HIPCHK(hipEventCreateWithFlags(&r->done[k], hipEventDisableTiming));
   }
   *out = r.release();
   return BDPT_OK;
@@ -236,22 +254,37 @@ int bdpt_reduce_frames(bdpt_reducer* r, int32_t root) {
     }
     s_eye[k] = se; s_light[k] = sl; s_count[k] = sc;
   }
-  // the collective: one group, each rank's reduces on its lead stream, into the root's frames
+  // the collective: one group, each rank's reduces on its lead stream, into the root's frames.
+  // The group is always closed, also when an enqueue fails (an open group would defer every later
+  // RCCL call of this thread); the first failure is what the call reports.
   NCCLCHK(L.GroupStart());
-  for (int k = 0; k < nr; k++) {
+  ncclResult_t first = ncclSuccess;
+  const char* what = "";
+  auto note = [&](ncclResult_t e, const char* call) {
+    if (e != ncclSuccess && first == ncclSuccess) { first = e; what = call; }
+  };
+  for (int k = 0; k < nr && first == ncclSuccess; k++) {
     hipStream_t st = r->ctxs[lead[k]]->stream;
     const bool at_root = k == root_rank;
-    NCCLCHK(L.Reduce(s_eye[k], at_root ? R->d_eye : nullptr, (size_t)n3, ncclFloat32, ncclSum, root_rank, r->comms[k], st));
-    NCCLCHK(L.Reduce(s_light[k], at_root ? R->d_light : nullptr, (size_t)n3, ncclFloat32, ncclSum, root_rank, r->comms[k], st));
+    note(L.Reduce(s_eye[k], at_root ? R->d_eye : nullptr, (size_t)n3, ncclFloat32, ncclSum, root_rank, r->comms[k], st),
+         "ncclReduce (eye frame)");
+    note(L.Reduce(s_light[k], at_root ? R->d_light : nullptr, (size_t)n3, ncclFloat32, ncclSum, root_rank, r->comms[k], st),
+         "ncclReduce (light frame)");
     if (r->pt)
-      NCCLCHK(L.Reduce(s_count[k], at_root ? R->d_count : nullptr, (size_t)np, ncclInt32, ncclSum, root_rank, r->comms[k], st));
+      note(L.Reduce(s_count[k], at_root ? R->d_count : nullptr, (size_t)np, ncclInt32, ncclSum, root_rank, r->comms[k], st),
+           "ncclReduce (sample counts)");
   }
-  NCCLCHK(L.GroupEnd());
+  note(L.GroupEnd(), "ncclGroupEnd");
+  if (first != ncclSuccess) {
+    g_err = std::string("RCCL ") + what + ": " + L.GetErrorString(first);
+    return BDPT_E_DEVICE;
+  }
   // later work on any member (a clear, the next render) is ordered after the reduce read its frames
   for (int k = 0; k < nr; k++) {
     Ctx* l = r->ctxs[lead[k]];
     HIPCHK(hipSetDevice(r->devs[k]));
     HIPCHK(hipEventRecord(r->ev[lead[k]], l->stream));
+    HIPCHK(hipEventRecord(r->done[k], l->stream));
     for (int i : r->members[k])
       if (i != lead[k]) HIPCHK(hipStreamWaitEvent(r->ctxs[i]->stream, r->ev[lead[k]], 0));
   }
@@ -270,9 +303,12 @@ int bdpt_reduce_rccl_version(void) {
 
 void bdpt_reduce_destroy(bdpt_reducer* r) {
   if (!r) return;
-  for (size_t k = 0; k < r->devs.size(); k++) {   // finish what was enqueued before freeing
+  // finish the last reduce (its device sums and collectives, which use the scratch freed below)
+  // through the reducer's own events: the contexts may already be destroyed (bdpt_destroy syncs
+  // its stream first, so their part of the work has completed then)
+  for (size_t k = 0; k < r->devs.size(); k++) {
     (void)hipSetDevice(r->devs[k]);
-    for (int i : r->members[k]) (void)hipStreamSynchronize(r->ctxs[i]->stream);
+    if (r->done[k]) (void)hipEventSynchronize(r->done[k]);
   }
   free_reducer(r);
 }

@@ -240,14 +240,19 @@ int main(int argc, char** argv) {
   };
   if (!run(0)) { cleanup(); return 1; }
   // the frame reduce over the N contexts (RCCL, bdpt_reduce_*): its communicator is set up here,
-  // outside the timer like the contexts; the reduce itself runs inside it
-  if (bdpt_reduce_create(ctxs.data(), gpus, &red) != BDPT_OK) { fail("creating the frame reduce"); cleanup(); return 1; }
+  // outside the timer like the contexts; the reduce itself runs inside it. One context holds the
+  // whole frame already: -g 1 needs neither RCCL nor a reduce.
+  if (gpus > 1 && bdpt_reduce_create(ctxs.data(), gpus, &red) != BDPT_OK) {
+    fail("creating the frame reduce");
+    cleanup();
+    return 1;
+  }
   std::vector<float> img((size_t)w * h * 3, 0.0f);
   std::vector<int32_t> count((size_t)w * h, 0);
   auto t0 = std::chrono::steady_clock::now();
   if (!run(1)) { cleanup(); return 1; }
   // every device's partial frame summed into context 0's over xGMI, then one read-back
-  if (bdpt_reduce_frames(red, 0) != BDPT_OK || bdpt_read_frame(ctxs[0], BDPT_FRAME_SAMPLE, img.data()) != BDPT_OK ||
+  if ((red && bdpt_reduce_frames(red, 0) != BDPT_OK) || bdpt_read_frame(ctxs[0], BDPT_FRAME_SAMPLE, img.data()) != BDPT_OK ||
       bdpt_read_sample_counts(ctxs[0], count.data()) != BDPT_OK) {
     fail("reducing the frames");
     cleanup();

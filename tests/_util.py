@@ -104,6 +104,22 @@ def oracle_pt_render(scene, W, H, spp, max_depth, mode, seed=5489, ns_area_light
     return img, cnt, st
 
 
+_ndev = None
+
+
+def device_count() -> int:
+    """Visible GPUs (torch.cuda.device_count(), which counts without initialising HIP on this
+    image); 0 in the CPU container. The >= 2-device tests skip below 2."""
+    global _ndev
+    if _ndev is None:
+        try:
+            import torch
+            _ndev = int(torch.cuda.device_count())
+        except Exception:
+            _ndev = 0
+    return _ndev
+
+
 def golden_scene(name, width=None, height=None):
     sc = B.scene_from_json(os.path.join(GOLD, "scenes", name + ".json"))
     if width is not None:

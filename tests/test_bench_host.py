@@ -32,3 +32,92 @@ def test_reference_baseline_reports_both_thread_counts():
     assert r["cores"] == int(best)
     assert abs(r["value"] - tried[best]["value"]) <= 1e-5 * max(1.0, r["value"])
     assert r["spp1"]["value"] > 0 and "-t 1 / -t 2" in r["sample"]
+
+
+# --- bench.py --gpus N: the launch plan, decided before any GPU call (plan_launch) ----------------
+
+def test_plan_single_and_inprocess():
+    assert bench.plan_launch(1, None, None, 1) == {"mode": "single", "world": 1, "devices": [0]}
+    p = bench.plan_launch(4, None, None, 8)
+    assert p["mode"] == "inprocess" and p["world"] == 4 and p["devices"] == [0, 1, 2, 3]
+    p = bench.plan_launch(2, None, "0,0", 1)     # two contexts sharing the one GPU of a test box
+    assert p["mode"] == "inprocess" and p["devices"] == [0, 0]
+    p = bench.plan_launch(8, None, None, 8)
+    assert p["devices"] == list(range(8))
+
+
+@pytest.mark.parametrize("gpus,ws,devs,ndev,msg", [
+    (2, None, None, 1, "only 1 visible"),          # too few devices for the default placement
+    (8, None, None, 0, "only 0 visible"),
+    (2, None, "0,1", 1, "needs device 1"),         # --devices names a device that is not there
+    (2, None, "0", 2, "lists 1 devices"),          # --devices of the wrong length
+    (1, None, "0,0", 1, "lists 2 devices"),
+    (2, "4", None, 8, "WORLD_SIZE=4"),             # torchrun world size disagrees with --gpus
+    (1, "2", None, 8, "WORLD_SIZE=2"),
+    (0, None, None, 8, "< 1"),
+    (2, None, "0,-1", 8, "negative device"),
+])
+def test_plan_rejects_mismatches(gpus, ws, devs, ndev, msg):
+    with pytest.raises(SystemExit) as e:
+        bench.plan_launch(gpus, ws, devs, ndev)
+    assert msg in str(e.value)
+    assert e.value.code not in (0, None)        # a message code: the process exits non-zero
+
+
+def test_plan_torchrun_keeps_the_device_map():
+    p = bench.plan_launch(2, "2", "0,0", 0)
+    assert p == {"mode": "torchrun", "world": 2, "devmap": [0, 0]}
+    assert bench.plan_launch(8, "8", None, 0)["devmap"] is None
+
+
+def test_main_rejects_too_few_devices_before_touching_a_gpu():
+    """The whole script, as the driver runs it: --gpus 2 with no launcher and no visible GPU (this
+    container) exits non-zero with the reason and prints no JSON line."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-parity",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert "only 0 visible" in r.stderr and not r.stdout.strip()
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "must agree" in r.stderr
+
+
+# --- product knobs in the environment ---------------------------------------------------------
+
+def test_knobs_recorded_and_refused_for_named_workloads():
+    env = {"BDPT_LDS_MODE": "0", "BDPT_PHASES": "1", "PATH": "/bin"}
+    assert bench.knob_env(env) == {"BDPT_LDS_MODE": "0", "BDPT_PHASES": "1"}
+    with pytest.raises(SystemExit) as e:
+        bench.check_knobs(env, named=True)
+    assert "BDPT_LDS_MODE=0" in str(e.value)
+    bench.check_knobs(env, named=False)                       # a custom configuration may measure it
+    bench.check_knobs({"BDPT_PHASES": "1"}, named=True)       # tooling variables do not change the product
+    for k in bench.PRODUCT_KNOBS:
+        with pytest.raises(SystemExit):
+            bench.check_knobs({k: "1"}, named=True)
+
+
+def test_product_knobs_cover_every_getenv_of_the_library():
+    """Every getenv in the product sources is a PRODUCT_KNOB (so none can change the headline
+    silently)."""
+    import re
+    names = set()
+    csrc = os.path.join(REPO, "bidirectional-pathtracing_amd", "csrc")
+    for f in os.listdir(csrc):
+        with open(os.path.join(csrc, f), errors="replace") as fh:
+            text = fh.read()
+        names |= set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', text))
+        names |= set(re.findall(r'env_int\("([A-Z0-9_]+)"', text))
+    assert names and names <= set(bench.PRODUCT_KNOBS), names - set(bench.PRODUCT_KNOBS)
+
+
+def test_main_refuses_a_knob_on_the_headline():
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BDPT_SAH_BINS"] = "32"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode != 0 and "BDPT_SAH_BINS=32" in r.stderr and not r.stdout.strip()

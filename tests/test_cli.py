@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from _util import MODE_C32, REPO, golden_scene, oracle_render
+from _util import MODE_C32, REPO, device_count, golden_scene, oracle_render
 from test_output_stage import CLI, read_png
 
 pytestmark = pytest.mark.gpu
@@ -136,7 +136,8 @@ def test_cli_multi_gpu_split(tmp_path, gpus, spp):
     frames summed by the C-ABI's reduce (bdpt_reduce_frames: on-device sum of the contexts sharing a
     GPU, then the RCCL ncclReduce, inside the timed region). --devices puts every worker on device 0
     so a one-GPU box runs the N-worker path; the image must match one render of all samples (oracle
-    mode 2). (-g 1, test_cli_renders_scene_like_oracle, goes through a one-rank RCCL reduce.)"""
+    mode 2). (-g 1, test_cli_renders_scene_like_oracle, makes no reducer: one context holds the
+    whole frame, so a one-GPU render needs no RCCL.)"""
     W, H, M = 64, 48, 5
     out = tmp_path / "g.png"
     r = subprocess.run([CLI, "-s", str(spp), "-m", str(M), "-r", str(W), str(H), "-g", str(gpus), "--devices",
@@ -150,4 +151,23 @@ def test_cli_multi_gpu_split(tmp_path, gpus, spp):
     np.ascontiguousarray(ref_hdr, dtype="<f8").tofile(raw)
     subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
     d = np.abs(ours.astype(int) - read_png(tmp_path / "ref.png").astype(int))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size
+
+
+@pytest.mark.skipif(device_count() < 2, reason="needs >= 2 visible GPUs (every box of this pool has one): "
+                                               "-g 2 on distinct devices = a two-rank RCCL reduce over xGMI")
+def test_cli_two_devices_default_placement(tmp_path):
+    """-g 2 with the default placement (worker g on device g): two RCCL ranks, the cross-device
+    ncclReduce of bdpt_reduce_frames into device 0's frames. Same image bar as the one-device split."""
+    W, H, M, spp = 64, 48, 5, 4
+    out = tmp_path / "g2.png"
+    r = subprocess.run([CLI, "-s", str(spp), "-m", str(M), "-r", str(W), str(H), "-g", "2", "-f", str(out),
+                        os.path.join(REPO, "scenes", "CBspheres.dae")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "2 GPU(s)" in r.stderr
+    ref_hdr = oracle_render(golden_scene("CBspheres", W, H), W, H, spp, M, MODE_C32)[0]
+    raw = tmp_path / "ref.f64"
+    np.ascontiguousarray(ref_hdr, dtype="<f8").tofile(raw)
+    subprocess.run([CLI, "--tonemap", str(raw), str(W), str(H), str(tmp_path / "ref.png")], check=True)
+    d = np.abs(read_png(out).astype(int) - read_png(tmp_path / "ref.png").astype(int))
     assert d.max() <= 1 and np.count_nonzero(d) <= 0.002 * d.size

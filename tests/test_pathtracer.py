@@ -20,7 +20,8 @@ from _util import MODE_C32, MODE_REF, REPO, oracle_pt_render
 
 PT = os.path.join(REPO, "tests", "golden", "pt")
 NAMES = ["lambertian", "delta", "microfacet", "roulette", "hemisphere", "env_lens", "adaptive",
-         "bunny_microfacet", "ambient", "ambient_microfacet_env", "directional_ambient", "directional"]
+         "bunny_microfacet", "ambient", "ambient_microfacet_env", "directional_ambient", "directional",
+         "batch_rounding"]
 
 
 def _load(name):
@@ -40,6 +41,19 @@ def test_oracle_mode0_bit_exact_vs_reference_pathtracer(name):
     img, cnt, _ = oracle_pt_render(sc, W, H, spp, M, MODE_REF, threads=1, **kw)
     assert np.array_equal(cnt, g["counts"])
     assert np.array_equal(img, g["image"]), np.abs(img - g["image"]).max()
+
+
+def test_batch_rounded_sample_counts():
+    """ns_aa 4 below samplesPerBatch 32: the reference runs one whole batch and records
+    num_samples = 32 for every pixel (pathtracer.cpp:301-337) — the reference's own counts
+    (fixture batch_rounding, ref_driver -U) and oracle mode 0 agree on it, and so does mode 2 (the
+    device semantics); tests/test_gpu_reduce.py asserts the same value for the GPU's reduced counts."""
+    sc, g, W, H, spp, M, kw = _load("batch_rounding")
+    assert spp == 4 and kw["batch"] == 32
+    assert (g["counts"] == 32).all()
+    for mode in (MODE_REF, MODE_C32):
+        _, cnt, _ = oracle_pt_render(sc, W, H, spp, M, mode, threads=4, **kw)
+        assert (cnt == 32).all()
 
 
 _core = None

@@ -8,7 +8,7 @@ oracle/_ref/ref_driver -U at -t 1 (bit-deterministic), for SURVEY.md §8 row f4:
   tests/golden/scenes/{banana,teapot}.compact.json : the loader dumps of the directional-light scenes
     (geometry as sha256 of its canonical JSON).
 Run in this container (needs /root/reference and `make -f oracle/ref.mk`).
-usage: python tools/make_pt_golden.py
+usage: python tools/make_pt_golden.py [config ...]   (default: every config)
 """
 import hashlib
 import json
@@ -40,6 +40,9 @@ CONFIGS = {
     # DirectionalLight (light.cpp:11-23): dae/keenan/banana.dae (+ ambient), dae/meshedit/teapot.dae
     "directional_ambient": ("banana", 48, 36, 2, 3, dict(batch=2, tol=0.05, nal=2)),
     "directional": ("teapot", 48, 36, 4, 4, dict(batch=4, tol=0.05)),
+    # ns_aa below samplesPerBatch: the reference still runs one whole batch, so every pixel records
+    # num_samples = 32 (pathtracer.cpp:301-337); the rule the GPU reduce's count test asserts
+    "batch_rounding": ("CBspheres", 48, 36, 4, 5, dict(batch=32, tol=0.0)),
 }
 # loader dumps too large to keep whole: lights, materials and camera verbatim, the geometry hashed
 COMPACT_DUMPS = ["banana", "teapot"]
@@ -68,6 +71,8 @@ def main():
             with open(os.path.join(REPO, "tests", "golden", "scenes", name + ".compact.json"), "w") as f:
                 json.dump(dump, f, indent=1)
         for name, (scene, W, H, spp, M, st) in CONFIGS.items():
+            if len(sys.argv) > 1 and name not in sys.argv[1:]:
+                continue
             pre = os.path.join(tmp, name)
             cmd = [DRV, "-U", "-t", "1", "-s", str(spp), "-m", str(M), "-r", str(W), str(H),
                    "-a", str(st["batch"]), str(st["tol"]), "-l", str(st.get("nal", 1)), "-o", pre]
