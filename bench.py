@@ -282,7 +282,8 @@ def load_traffic(workload: str, kernel_ms: float):
 # of them set, so the line always states the product configuration; every BDPT_* variable that is
 # set goes into config.env.
 PRODUCT_KNOBS = ("BDPT_LDS_MODE", "BDPT_NTOP_MAX", "BDPT_BLOCK_MAJOR", "BDPT_XCD_GROUPS",
-                 "BDPT_BVH", "BDPT_SAH_LEAF", "BDPT_SAH_CT", "BDPT_SAH_BINS")
+                 "BDPT_BVH", "BDPT_SAH_LEAF", "BDPT_SAH_CT", "BDPT_SAH_BINS", "BDPT_SBVH",
+                 "BDPT_SBVH_BUDGET")
 
 
 def knob_env(environ) -> dict:

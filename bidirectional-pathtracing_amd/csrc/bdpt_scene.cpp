@@ -105,11 +105,19 @@ struct Builder {
 };
 
 // Device tree: binned SAH (16 bins per axis on centroid bounds, leaves of <= 2 primitives with SAH
-// termination; the leaf encoding allows up to 4). Which tree the device traverses does not change any result: closest
+// termination; the leaf encoding allows up to 4), optionally with spatial splits (SBVH, Stich et
+// al. 2009: a triangle straddling a split plane is referenced from both sides, each side bounding
+// only its clipped part). Which tree the device traverses does not change any result: closest
 // hits are decided by t, ties by the primitive's position in the REFERENCE tree's DFS leaf order
-// (the reference keeps the last of equal-t hits, bvh.cpp:161-188), and any-hit is order free.
+// (the reference keeps the last of equal-t hits, bvh.cpp:161-188; a primitive referenced twice
+// gives the same t and key both times), and any-hit is order free.
 struct SahBuilder {
+  struct Ref {
+    int prim;
+    Box box;   // the part of the primitive this reference bounds (its whole box unless clipped)
+  };
   const std::vector<Box>* pb;
+  const bdpt_scene_desc* desc = nullptr;   // triangle vertices for the spatial-split clipping
   std::vector<Node> nodes;
   std::vector<int> leaf_prims;
   int depth = 0;
@@ -122,89 +130,219 @@ struct SahBuilder {
   double ct = 1.0;
   int nb = 16;          // centroid bins per axis (<= kMaxBins)
   static constexpr int kMaxBins = 64;
+  // spatial splits: tried at a node when its best object split's children overlap by more than
+  // alpha x the root's area; at most budget x n references in all (0 = off)
+  double alpha = 0;
+  double budget = 0;
+  int nsb = 32;         // spatial bins per axis (<= kMaxBins)
+  size_t max_refs = 0, nrefs = 0;
+  double root_area = 0;
   static double area(const Box& b) {
     const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
     return dx < 0 ? 0 : 2 * (dx * dy + dy * dz + dz * dx);
   }
-  int make_leaf(const int* prims, int n) {
+  static Box empty_box() {
+    Box b;
+    for (int k = 0; k < 3; k++) { b.mn[k] = INFINITY; b.mx[k] = -INFINITY; }
+    return b;
+  }
+  static Box intersect(const Box& a, const Box& b) {
+    Box r;
+    for (int k = 0; k < 3; k++) { r.mn[k] = std::max(a.mn[k], b.mn[k]); r.mx[k] = std::min(a.mx[k], b.mx[k]); }
+    return r;
+  }
+  static bool valid(const Box& b) { return b.mn[0] <= b.mx[0] && b.mn[1] <= b.mx[1] && b.mn[2] <= b.mx[2]; }
+  // the box of the part of reference r within [lo, hi] along axis ax: a triangle is clipped as a
+  // polygon (its vertices inside the slab and its edges' crossings of the two planes), anything
+  // else by its box; the result is also within r's own box (earlier clips)
+  Box clip(const Ref& r, int ax, double lo, double hi) const {
+    Box b = empty_box();
+    if (desc->prim_type[r.prim] == BDPT_PRIM_TRIANGLE) {
+      const double* g = desc->prim_geom + 18 * (size_t)r.prim;
+      for (int e = 0; e < 3; e++) {
+        const double* a = g + 3 * e;
+        const double* c = g + 3 * ((e + 1) % 3);
+        if (a[ax] >= lo && a[ax] <= hi) b.expand_pt(a);
+        for (double pl : {lo, hi}) {
+          if ((a[ax] < pl && c[ax] > pl) || (a[ax] > pl && c[ax] < pl)) {
+            const double t = (pl - a[ax]) / (c[ax] - a[ax]);
+            double q[3];
+            for (int k = 0; k < 3; k++) q[k] = a[k] + t * (c[k] - a[k]);
+            q[ax] = pl;
+            b.expand_pt(q);
+          }
+        }
+      }
+    } else {
+      b = (*pb)[r.prim];
+    }
+    Box slab = r.box;
+    slab.mn[ax] = std::max(slab.mn[ax], lo);
+    slab.mx[ax] = std::min(slab.mx[ax], hi);
+    return intersect(b, slab);
+  }
+  int make_leaf(const Ref* refs, int n) {
     Node nd;
-    nd.box = (*pb)[prims[0]];
-    for (int k = 0; k < n; k++) nd.box.expand((*pb)[prims[k]]);
+    nd.box = refs[0].box;
+    for (int k = 0; k < n; k++) nd.box.expand(refs[k].box);
     nd.start = (int)leaf_prims.size();
     nd.count = n;
-    for (int k = 0; k < n; k++) leaf_prims.push_back(prims[k]);
+    for (int k = 0; k < n; k++) leaf_prims.push_back(refs[k].prim);
     nodes.push_back(nd);
     return (int)nodes.size() - 1;
   }
-  int build(int* prims, int n, int d) {
+  int build_root(int n) {
+    std::vector<Ref> refs(n);
+    for (int i = 0; i < n; i++) refs[i] = Ref{i, (*pb)[i]};
+    Box all = refs[0].box;
+    for (int i = 1; i < n; i++) all.expand(refs[i].box);
+    root_area = area(all);
+    nrefs = (size_t)n;
+    max_refs = (size_t)((double)n * (1.0 + std::max(0.0, budget)));
+    return build(refs, 0);
+  }
+  int build(std::vector<Ref>& refs, int d) {
     depth = std::max(depth, d);
-    const auto& B = *pb;
-    if (n <= 1 || (n <= leaf_max && ct <= 0)) return make_leaf(prims, n);
-    Box cb;
-    for (int k = 0; k < 3; k++) { cb.mn[k] = INFINITY; cb.mx[k] = -INFINITY; }
+    const int n = (int)refs.size();
+    if (n <= 1 || (n <= leaf_max && ct <= 0)) return make_leaf(refs.data(), n);
+    Box cb = empty_box();
     for (int i = 0; i < n; i++) {
-      double c[3] = {B[prims[i]].centroid(0), B[prims[i]].centroid(1), B[prims[i]].centroid(2)};
+      double c[3] = {refs[i].box.centroid(0), refs[i].box.centroid(1), refs[i].box.centroid(2)};
       cb.expand_pt(c);
     }
     const int NB = nb;
     double best = INFINITY;
     int best_axis = -1, best_split = 0;
+    Box best_l, best_r;
     for (int ax = 0; ax < 3; ax++) {
       const double lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
       if (!(ext > 0)) continue;
       Box bb[kMaxBins];
       int cnt[kMaxBins] = {0};
-      for (int b = 0; b < NB; b++)
-        for (int k = 0; k < 3; k++) { bb[b].mn[k] = INFINITY; bb[b].mx[k] = -INFINITY; }
+      for (int b = 0; b < NB; b++) bb[b] = empty_box();
       for (int i = 0; i < n; i++) {
-        int b = (int)((B[prims[i]].centroid(ax) - lo) / ext * NB);
+        int b = (int)((refs[i].box.centroid(ax) - lo) / ext * NB);
         b = std::min(NB - 1, std::max(0, b));
         cnt[b]++;
-        bb[b].expand(B[prims[i]]);
+        bb[b].expand(refs[i].box);
       }
       double ra[kMaxBins];
       int rc[kMaxBins];
-      Box acc;
-      for (int k = 0; k < 3; k++) { acc.mn[k] = INFINITY; acc.mx[k] = -INFINITY; }
+      Box rb[kMaxBins];
+      Box acc = empty_box();
       int c = 0;
       for (int b = NB - 1; b > 0; b--) {
         acc.expand(bb[b]);
         c += cnt[b];
         ra[b] = area(acc);
         rc[b] = c;
+        rb[b] = acc;
       }
-      for (int k = 0; k < 3; k++) { acc.mn[k] = INFINITY; acc.mx[k] = -INFINITY; }
+      acc = empty_box();
       c = 0;
       for (int b = 0; b < NB - 1; b++) {
         acc.expand(bb[b]);
         c += cnt[b];
         if (c == 0 || rc[b + 1] == 0) continue;
         const double cost = area(acc) * c + ra[b + 1] * rc[b + 1];
-        if (cost < best) { best = cost; best_axis = ax; best_split = b + 1; }
+        if (cost < best) { best = cost; best_axis = ax; best_split = b + 1; best_l = acc; best_r = rb[b + 1]; }
       }
     }
     if (n <= leaf_max && ct > 0) {
-      Box nb = B[prims[0]];
-      for (int i = 1; i < n; i++) nb.expand(B[prims[i]]);
-      const double an = area(nb);
-      if (best_axis < 0 || !(an > 0) || (double)n <= ct + best / an) return make_leaf(prims, n);
+      Box nb_ = refs[0].box;
+      for (int i = 1; i < n; i++) nb_.expand(refs[i].box);
+      const double an = area(nb_);
+      if (best_axis < 0 || !(an > 0) || (double)n <= ct + best / an) return make_leaf(refs.data(), n);
     }
-    int nl;
-    if (best_axis < 0) {
-      nl = n / 2;   // coincident centroids: split in input order
-    } else {
-      const double lo = cb.mn[best_axis], ext = cb.mx[best_axis] - cb.mn[best_axis];
-      int* mid = std::stable_partition(prims, prims + n, [&](int p) {
-        int b = (int)((B[p].centroid(best_axis) - lo) / ext * NB);
-        return std::min(NB - 1, std::max(0, b)) < best_split;
-      });
-      nl = (int)(mid - prims);
-      if (nl == 0 || nl == n) nl = n / 2;
+    // spatial split: only where the object split's children overlap and the reference budget lasts
+    int sp_axis = -1;
+    double sp_pos = 0;
+    if (alpha > 0 && n > leaf_max && nrefs < max_refs && best_axis >= 0) {
+      const Box ov = intersect(best_l, best_r);
+      if (valid(ov) && area(ov) > alpha * root_area) {
+        Box nbx = refs[0].box;
+        for (int i = 1; i < n; i++) nbx.expand(refs[i].box);
+        const int SB = nsb;
+        double sbest = best;
+        for (int ax = 0; ax < 3; ax++) {
+          const double lo = nbx.mn[ax], ext = nbx.mx[ax] - nbx.mn[ax];
+          if (!(ext > 0)) continue;
+          Box bb[kMaxBins];
+          int ent[kMaxBins] = {0}, ex[kMaxBins] = {0};
+          for (int b = 0; b < SB; b++) bb[b] = empty_box();
+          auto bin_of = [&](double v) { return std::min(SB - 1, std::max(0, (int)((v - lo) / ext * SB))); };
+          for (int i = 0; i < n; i++) {
+            const int b0 = bin_of(refs[i].box.mn[ax]), b1 = bin_of(refs[i].box.mx[ax]);
+            ent[b0]++;
+            ex[b1]++;
+            for (int b = b0; b <= b1; b++) {
+              const Box cbx = b0 == b1 ? refs[i].box
+                                       : clip(refs[i], ax, lo + ext * b / SB, b + 1 == SB ? nbx.mx[ax] : lo + ext * (b + 1) / SB);
+              if (valid(cbx)) bb[b].expand(cbx);
+            }
+          }
+          double ra[kMaxBins];
+          int rc[kMaxBins];
+          Box acc = empty_box();
+          int c = 0;
+          for (int b = SB - 1; b > 0; b--) {
+            acc.expand(bb[b]);
+            c += ex[b];
+            ra[b] = area(acc);
+            rc[b] = c;
+          }
+          acc = empty_box();
+          c = 0;
+          for (int b = 0; b < SB - 1; b++) {
+            acc.expand(bb[b]);
+            c += ent[b];
+            if (c == 0 || rc[b + 1] == 0) continue;
+            const double cost = area(acc) * c + ra[b + 1] * rc[b + 1];
+            if (cost < sbest) { sbest = cost; sp_axis = ax; sp_pos = lo + ext * (b + 1) / SB; }
+          }
+        }
+      }
     }
+    std::vector<Ref> left, right;
+    if (sp_axis >= 0) {
+      for (const Ref& r : refs) {
+        if (r.box.mx[sp_axis] <= sp_pos) { left.push_back(r); continue; }
+        if (r.box.mn[sp_axis] >= sp_pos) { right.push_back(r); continue; }
+        const Box lb = clip(r, sp_axis, -INFINITY, sp_pos), rbx = clip(r, sp_axis, sp_pos, INFINITY);
+        const bool lv = valid(lb), rv = valid(rbx);
+        if (lv) left.push_back(Ref{r.prim, lb});
+        if (rv) right.push_back(Ref{r.prim, rbx});
+        if (!lv && !rv) left.push_back(r);   // degenerate clip: keep the reference whole
+        if (lv && rv) nrefs++;
+      }
+      if (left.empty() || right.empty()) {   // nothing gained: fall back to the object split
+        nrefs -= left.size() + right.size() - refs.size();
+        left.clear();
+        right.clear();
+        sp_axis = -1;
+      }
+    }
+    if (sp_axis < 0) {
+      int nl;
+      if (best_axis < 0) {
+        nl = n / 2;   // coincident centroids: split in input order
+      } else {
+        const double lo = cb.mn[best_axis], ext = cb.mx[best_axis] - cb.mn[best_axis];
+        auto mid = std::stable_partition(refs.begin(), refs.end(), [&](const Ref& r) {
+          int b = (int)((r.box.centroid(best_axis) - lo) / ext * NB);
+          return std::min(NB - 1, std::max(0, b)) < best_split;
+        });
+        nl = (int)(mid - refs.begin());
+        if (nl == 0 || nl == n) nl = n / 2;
+      }
+      left.assign(refs.begin(), refs.begin() + nl);
+      right.assign(refs.begin() + nl, refs.end());
+    }
+    std::vector<Ref>().swap(refs);
     const int id = (int)nodes.size();
     nodes.push_back(Node());
-    const int l = build(prims, nl, d + 1);
-    const int r = build(prims + nl, n - nl, d + 1);
+    const int l = build(left, d + 1);
+    const int r = build(right, d + 1);
     Box bb = nodes[l].box;
     bb.expand(nodes[r].box);
     nodes[id].l = l;
@@ -420,13 +558,19 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
   if (!use_ref) {
     SahBuilder S;
     S.pb = &pb;
+    S.desc = d;
     // diagnostics / A-B: leaf size and SAH termination of the device tree (no effect on results)
     if (const char* e = getenv("BDPT_SAH_LEAF")) S.leaf_max = std::max(1, std::min(4, atoi(e)));
     if (const char* e = getenv("BDPT_SAH_CT")) S.ct = atof(e);
     if (const char* e = getenv("BDPT_SAH_BINS")) S.nb = std::max(2, std::min(SahBuilder::kMaxBins, atoi(e)));
-    std::vector<int> idx(n);
-    for (int i = 0; i < n; i++) idx[i] = i;
-    root = S.build(idx.data(), n, 0);
+    // spatial splits (scenes of >= kSbvhMinPrims primitives): alpha and the reference budget
+    if (n >= kSbvhMinPrims) {
+      S.alpha = kSbvhAlpha;
+      S.budget = kSbvhBudget;
+    }
+    if (const char* e = getenv("BDPT_SBVH")) S.alpha = n >= kSbvhMinPrims ? atof(e) : 0.0;
+    if (const char* e = getenv("BDPT_SBVH_BUDGET")) S.budget = atof(e);
+    root = S.build_root(n);
     Bs.nodes = std::move(S.nodes);
     Bs.leaf_prims = std::move(S.leaf_prims);
     Bs.depth = S.depth;
@@ -435,11 +579,14 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
   out.dev_depth = T.depth;
   out.dev_nodes = (int)T.nodes.size();
 
-  // primitives in the device tree's DFS leaf order
+  // primitives in the device tree's DFS leaf order (a primitive that a spatial split references
+  // from two leaves has a record at both positions)
+  const int nref = (int)T.leaf_prims.size();
+  if (nref >= (1 << 24)) { err = "too many primitive references for the leaf encoding (2^24)"; return BDPT_E_UNSUPPORTED; }
   out.prim_ref = T.leaf_prims;
-  out.geom.assign(12 * (size_t)n, 0.0f);
-  out.shade.assign(12 * (size_t)n, 0.0f);
-  for (int k = 0; k < n; k++) {
+  out.geom.assign(12 * (size_t)nref, 0.0f);
+  out.shade.assign(12 * (size_t)nref, 0.0f);
+  for (int k = 0; k < nref; k++) {
     int i = T.leaf_prims[k];
     const double* g = d->prim_geom + 18 * (size_t)i;
     float* G = &out.geom[12 * (size_t)k];

@@ -8,9 +8,10 @@
 //           node_bytes(W) record per node = the children's fp32 AABBs (outward-rounded and padded
 //           by 2^-16 of the box scale, so the fp32 slab test is conservative) + child refs; the
 //           layouts are at node_step (bdpt_core.h)
-//   geom  : 48 B per primitive in DFS leaf order (triangle p0,e1,e2 | sphere c,r)
-//   shade : 48 B per primitive (triangle n1,n2,n3 | sphere flag) + material id
-//   prim_ref: DFS position -> reference primitive index
+//   geom  : 48 B per primitive reference in DFS leaf order (triangle p0,e1,e2 | sphere c,r); a
+//           primitive referenced from two leaves (spatial splits) has a record at both positions
+//   shade : 48 B per primitive reference (triangle n1,n2,n3 | sphere flag) + material id
+//   prim_ref: DFS position -> scene primitive index
 #pragma once
 
 #include <stdint.h>
@@ -56,6 +57,14 @@ struct HostScene {
 };
 
 constexpr int kTopNodes = 1024;
+// Spatial splits in the device tree (SBVH, bdpt_scene.cpp SahBuilder): tried at a node whose best
+// object split leaves children overlapping by more than kSbvhAlpha x the root's surface area, up
+// to kSbvhBudget x n extra primitive references, in scenes of >= kSbvhMinPrims primitives (the
+// flat-list and all-in-LDS scenes stay unsplit). kSbvhAlpha 0 = off. Run-time A/B: BDPT_SBVH=alpha,
+// BDPT_SBVH_BUDGET=fraction.
+constexpr int kSbvhMinPrims = 256;
+constexpr double kSbvhAlpha = 0.0;
+constexpr double kSbvhBudget = 0.3;
 
 // LM 3's flat list as one run of primitives: when the device tree's leaves, in DFS order, hold
 // primitives 0, 1, ..., n-1 consecutively (the builder emits them so), returns n and sets *sph to

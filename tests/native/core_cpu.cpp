@@ -322,7 +322,8 @@ extern "C" int core_cpu_trace_rays(const bdpt_scene_desc* d, int lds_mode, const
 static std::vector<float> g_rays;
 extern "C" void core_cpu_ray_dump(int on) {
   g_rays.clear();
-  ray_dump() = on ? &g_rays : nullptr;
+  ray_dump() = on == 1 ? &g_rays : nullptr;          // 1: any-hit queries
+  ray_dump_closest() = on == 2 ? &g_rays : nullptr;  // 2: closest-hit queries
 }
 extern "C" long long core_cpu_ray_dump_get(float* out, long long max_rays) {
   const long long n = std::min<long long>(max_rays, (long long)g_rays.size() / 8);
