@@ -480,15 +480,18 @@ inline std::vector<float>*& ray_dump() { static thread_local std::vector<float>*
 // ... and the closest-hit queries' (tools/closest_probe.py)
 inline std::vector<float>*& ray_dump_closest() { static thread_local std::vector<float>* v = nullptr; return v; }
 #endif
-template <int K>
+// BOT (the cooperative traversals): entries can also be taken from the bottom (the oldest, highest
+// in the tree), pop_bottom; the memory part is then [lo, msp).
+template <int K, bool BOT = false>
 struct TravStack {
   int s[K > 0 ? K : 1];
   int nreg, msp;
+  int lo;     // BOT: first valid memory entry (0 otherwise)
   int* mem;   // a separate private array, so that s[] / nreg / msp stay in registers
   int* lds;   // this lane's LDS overflow slots (stride kLdsStackStride), or null
-  BDPT_HD explicit TravStack(int* m, int* l = nullptr) : nreg(0), msp(0), mem(m), lds(l) {}
-  BDPT_HD void clear() { nreg = 0; msp = 0; }
-  BDPT_HD int size() const { return nreg + msp; }
+  BDPT_HD explicit TravStack(int* m, int* l = nullptr) : nreg(0), msp(0), lo(0), mem(m), lds(l) {}
+  BDPT_HD void clear() { nreg = 0; msp = 0; lo = 0; }
+  BDPT_HD int size() const { return nreg + msp - (BOT ? lo : 0); }
   BDPT_HD void put(int k, int v) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if (kLdsStack > 0 && lds && k < kLdsStack) {
@@ -506,11 +509,16 @@ struct TravStack {
   }
   BDPT_HD void push(int v) {
     if (K == 0) {
+      if (BOT && msp == lo) { msp = 0; lo = 0; }
       put(msp++, v);
       return;
     }
-    if (nreg == K) put(msp++, s[K - 1]);
-    else nreg++;
+    if (nreg == K) {
+      if (BOT && msp == lo) { msp = 0; lo = 0; }
+      put(msp++, s[K - 1]);
+    } else {
+      nreg++;
+    }
 #pragma unroll
     for (int k = K - 1; k > 0; k--) s[k] = s[k - 1];
     s[0] = v;
@@ -523,9 +531,28 @@ struct TravStack {
       nreg--;
       return true;
     }
-    if (msp == 0) return false;
+    if (msp == (BOT ? lo : 0)) return false;
     v = get(--msp);
     return true;
+  }
+  // the oldest entry (BOT); the memory part only while its indices stay low (the array holds
+  // kStackMax entries and lo only grows until the memory part empties)
+  BDPT_HD bool can_pop_bottom() const { return size() > 0 && msp < kStackMax / 2; }
+  BDPT_HD bool pop_bottom(int& v) {
+    if (msp > lo) {
+      v = get(lo++);
+      if (lo == msp) { lo = 0; msp = 0; }
+      return true;
+    }
+    if (K > 0 && nreg > 0) {
+      v = s[0];
+#pragma unroll
+      for (int k = 1; k < K; k++)
+        if (k < nreg) v = s[k];
+      nreg--;
+      return true;
+    }
+    return false;
   }
 };
 
@@ -651,8 +678,8 @@ BDPT_HD void ld_node4_oct_lds(const float4* p, const RayInv& r, float4* v) {
 // fetched in near / far order per axis (ld_node4_oct_*)
 // ORD: visit hit children near-first (closest-hit queries); any-hit queries take them in slot order.
 // A child is entered when its slab interval, clipped to [tmin, tmax], is non-empty.
-template <int K, int LM, int ORD = 1>
-BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K>& stk,
+template <int K, int LM, int ORD = 1, bool BOT = false>
+BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, float tmax, TravStack<K, BOT>& stk,
                       Counters& c) {
   constexpr int W = lm_width(LM), NU = node_used_f4(W);
   float4 v[NU];
@@ -1052,273 +1079,6 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Cooperative traversal (lane donation). The wave pays for its slowest lane: a walk query takes ~6
-// node steps on average but the wave iterates ~27 (the tail of the per-query distribution,
-// DESIGN.md §5). Here the lanes whose query has finished take over pending subtrees of the lanes
-// still tracing: whenever at most kCoopThresh lanes still trace, every tracing lane with a non-empty
-// stack hands its top entry (with its ray and its current best distance) to an idle lane, which
-// traverses that subtree with a stack of its own and merges its closest hit back into the owner's
-// (a readlane per field). The candidate set of every query is unchanged and the merge keeps the
-// tie rule (smaller t, then the larger reference-tree key), so the result is the same bits as
-// trace_closest. Every lane of the wave must call it together (`have` = this lane has a query).
-constexpr int kCoopThresh = 16;
-
-BDPT_HD bool hit_better(float t, int key, float bt, int bkey) { return t < bt || (t == bt && key > bkey); }
-
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ int coop_bperm(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-__device__ __forceinline__ float coop_bperm(int src, float v) {
-  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
-}
-__device__ __forceinline__ int lanes_below_ull(unsigned long long m) {   // set bits of m below this lane
-  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-__device__ __forceinline__ int coop_readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float coop_readlane(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-// position of the k-th (0-based) set bit of m (k < popcount(m))
-__device__ __forceinline__ int select_kth(unsigned long long m, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int cnt = __popcll(m & ((1ull << w) - 1));
-    if (k >= cnt) { k -= cnt; m >>= w; pos += w; }
-  }
-  return pos;
-}
-#endif
-
-template <int LM = 0, int K = 0>
-BDPT_HD bool trace_closest_coop(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Hit& h, Counters& c,
-                                bool have) {
-#if !defined(__HIP_DEVICE_COMPILE__)
-  if (!have) return false;   // the host build runs one lane: nothing to share
-  return trace_closest<LM, K>(S, o, d, tmin, tmax, h, c);
-#else
-  static_assert(spec_trav(LM), "the cooperative traversal is the speculative while-while of LM 0 / 2");
-  const int lane = (int)__lane_id();
-  RayInv r = make_rayinv(o, d);   // the ray this lane works on (its own, or a borrowed one)
-  float wtmin = tmin;
-  Hit w;                          // the closest hit of the current work unit
-  w.t = tmax; w.prim = -1; w.key = -1; w.b1 = 0; w.b2 = 0;
-  Hit mine = w;                   // this lane's own query, with its helpers' hits merged in
-  int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem, lane_stack(S));
-  int ref = have ? S.root : kTravDone;
-  int pend = 0;
-  int owner = have ? lane : -1;   // whose query the current work unit belongs to; -1 = idle
-  if (have) c.closest++;
-  float4 a0, a1, a2;
-  auto test_leaf = [&](int lf) {
-    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
-    a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
-    for (int k = 0; k < cnt; k++) {
-      BDPT_LANE_PROF(c, LP_CPRIM);
-      const int pi = st + k;
-      float t, b1 = 0, b2 = 0;
-      bool ok;
-      int key;
-      const float4 g0 = a0, g1 = a1, g2 = a2;
-      const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
-      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
-      if ((sm >> k) & 1) {
-        c.sphs++;
-        ok = sph_test(g0, r.o, r.d, wtmin, w.t, &t);
-        key = __float_as_int(g1.x);
-      } else {
-        c.tris++;
-        ok = tri_test(g0, g1, g2, r.o, r.d, wtmin, w.t, &t, &b1, &b2);
-        key = __float_as_int(g2.y);
-      }
-      if (ok && (t < w.t || key > w.key)) {
-        w.t = t; w.prim = pi; w.key = key; w.b1 = b1; w.b2 = b2;
-      }
-    }
-  };
-  for (;;) {
-    // speculative while-while over the current work units (as trace_closest)
-    while (ref >= 0) {
-      BDPT_LANE_PROF(c, LP_CNODE);
-      ref = node_step<K, LM, kClosestOrd>(S, r, ref, wtmin, w.t, stk, c);
-      if (ref < 0 && ref != kTravDone && pend == 0) {
-        pend = ref;
-        if (!stk.pop(ref)) ref = kTravDone;
-      }
-      if (wave_count(pend == 0 && ref >= 0) == 0) break;
-    }
-    while (pend != 0) {
-      test_leaf(pend);
-      pend = 0;
-      if (ref < 0 && ref != kTravDone) {
-        pend = ref;
-        if (!stk.pop(ref)) ref = kTravDone;
-      }
-    }
-    // work units that ended: an own unit merges into `mine`, a borrowed one into its owner's
-    const bool fin = owner >= 0 && ref == kTravDone;
-    const bool own_working = owner == lane && !fin;
-    if (fin && owner == lane && w.prim >= 0 && hit_better(w.t, w.key, mine.t, mine.key)) mine = w;
-    unsigned long long mm = __ballot(fin && owner != lane && w.prim >= 0);
-    while (mm) {
-      const int hl = __builtin_ctzll(mm);
-      mm &= mm - 1;
-      const int ow = coop_readlane(owner, hl), hk = coop_readlane(w.key, hl), hp = coop_readlane(w.prim, hl);
-      const float ht = coop_readlane(w.t, hl), hb1 = coop_readlane(w.b1, hl), hb2 = coop_readlane(w.b2, hl);
-      if (lane == ow) {
-        if (own_working) {   // still tracing its own query: the hit also tightens its pruning
-          if (hit_better(ht, hk, w.t, w.key)) { w.t = ht; w.key = hk; w.prim = hp; w.b1 = hb1; w.b2 = hb2; }
-        } else if (hit_better(ht, hk, mine.t, mine.key)) {
-          mine.t = ht; mine.key = hk; mine.prim = hp; mine.b1 = hb1; mine.b2 = hb2;
-        }
-      }
-    }
-    if (fin) owner = -1;
-    const unsigned long long mW = __ballot(owner >= 0);
-    if (mW == 0) break;
-    if (__popcll(mW) > kCoopThresh) continue;
-    // donation: each tracing lane with a pending subtree hands its top stack entry to an idle lane
-    const unsigned long long mI = ~mW & __ballot(true), mD = __ballot(owner >= 0 && stk.size() > 0);
-    if (mI == 0 || mD == 0) continue;
-    const int ki = lanes_below_ull(mI), kd = lanes_below_ull(mD);
-    const bool take = owner < 0 && ki < __popcll(mD);
-    const bool give = owner >= 0 && stk.size() > 0 && kd < __popcll(mI);
-    int e = kTravDone;
-    if (give) stk.pop(e);
-    const int src = take ? select_kth(mD, ki) : lane;
-    const int e_in = coop_bperm(src, e), ow_in = coop_bperm(src, owner);
-    const float t_in = coop_bperm(src, w.t), tmin_in = coop_bperm(src, wtmin);
-    RayInv rin;
-    rin.o = mk3(coop_bperm(src, r.o.x), coop_bperm(src, r.o.y), coop_bperm(src, r.o.z));
-    rin.d = mk3(coop_bperm(src, r.d.x), coop_bperm(src, r.d.y), coop_bperm(src, r.d.z));
-    rin.inv = mk3(coop_bperm(src, r.inv.x), coop_bperm(src, r.inv.y), coop_bperm(src, r.inv.z));
-    rin.oi = mk3(coop_bperm(src, r.oi.x), coop_bperm(src, r.oi.y), coop_bperm(src, r.oi.z));
-    const int nn = coop_bperm(src, r.nx | (r.ny << 8) | (r.nz << 16));
-    if (take) {
-      r = rin;
-      r.nx = nn & 0xff; r.ny = (nn >> 8) & 0xff; r.nz = (nn >> 16) & 0xff;
-      wtmin = tmin_in;
-      w.t = t_in; w.prim = -1; w.key = -1; w.b1 = 0; w.b2 = 0;
-      owner = ow_in;
-      stk.clear();
-      if (e_in >= 0) { ref = e_in; pend = 0; }
-      else { pend = e_in; ref = kTravDone; }   // a leaf entry: tested in the next leaf phase
-    }
-  }
-  h = mine;
-  if (h.prim >= 0) c.hits++;
-  return h.prim >= 0;
-#endif
-}
-
-// Any hit, cooperatively (as trace_closest_coop): a borrowed subtree that holds a hit answers its
-// owner's query; a work unit whose owner's query is answered is dropped.
-template <int LM = 0, int K = 0>
-BDPT_HD bool trace_any_coop(const SceneView& S, f3 o, f3 d, float tmin, float tmax, Counters& c, bool have) {
-#if !defined(__HIP_DEVICE_COMPILE__)
-  if (!have) return false;
-  return trace_any<LM, K>(S, o, d, tmin, tmax, c);
-#else
-  static_assert(spec_trav(LM), "the cooperative traversal is the speculative while-while of LM 0 / 2");
-  const int lane = (int)__lane_id();
-  RayInv r = make_rayinv(o, d);
-  float wtmin = tmin, wtmax = tmax;
-  bool whit = false;   // the current work unit found a hit
-  bool mine = false;   // this lane's own query is answered (occluded)
-  int stack_mem[kStackMax];
-  TravStack<K> stk(stack_mem, lane_stack(S));
-  int ref = have ? S.root : kTravDone;
-  int pend = 0;
-  int owner = have ? lane : -1;
-  if (have) c.shadow++;
-  float4 a0, a1, a2;
-  auto test_leaf = [&](int lf) -> bool {
-    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
-    a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
-    for (int k = 0; k < cnt; k++) {
-      BDPT_LANE_PROF(c, LP_APRIM);
-      const int pi = st + k;
-      float t, b1, b2;
-      bool ok;
-      const float4 g0 = a0, g1 = a1, g2 = a2;
-      const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
-      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
-      if ((sm >> k) & 1) {
-        c.sphs++;
-        ok = sph_test(g0, r.o, r.d, wtmin, wtmax, &t);
-      } else {
-        c.tris++;
-        ok = tri_test(g0, g1, g2, r.o, r.d, wtmin, wtmax, &t, &b1, &b2);
-      }
-      if (ok) return true;
-    }
-    return false;
-  };
-  for (;;) {
-    while (ref >= 0) {
-      BDPT_LANE_PROF(c, LP_ANODE);
-      ref = node_step<K, LM, kAnyOrd>(S, r, ref, wtmin, wtmax, stk, c);
-      if (ref < 0 && ref != kTravDone && pend == 0) {
-        pend = ref;
-        if (!stk.pop(ref)) ref = kTravDone;
-      }
-      if (wave_count(pend == 0 && ref >= 0) == 0) break;
-    }
-    while (pend != 0) {
-      if (test_leaf(pend)) { whit = true; ref = kTravDone; pend = 0; break; }
-      pend = 0;
-      if (ref < 0 && ref != kTravDone) {
-        pend = ref;
-        if (!stk.pop(ref)) ref = kTravDone;
-      }
-    }
-    const bool fin = owner >= 0 && ref == kTravDone;
-    if (fin && owner == lane && whit) mine = true;
-    unsigned long long mm = __ballot(fin && owner != lane && whit);
-    while (mm) {
-      const int hl = __builtin_ctzll(mm);
-      mm &= mm - 1;
-      if (lane == coop_readlane(owner, hl)) mine = true;
-    }
-    // a unit still running whose owner's query is answered stops (its own lane's included)
-    const bool answered = coop_bperm(owner < 0 ? lane : owner, (int)mine) != 0;
-    if (fin || (owner >= 0 && answered)) { owner = -1; ref = kTravDone; pend = 0; }
-    const unsigned long long mW = __ballot(owner >= 0);
-    if (mW == 0) break;
-    if (__popcll(mW) > kCoopThresh) continue;
-    const unsigned long long mI = ~mW & __ballot(true), mD = __ballot(owner >= 0 && stk.size() > 0);
-    if (mI == 0 || mD == 0) continue;
-    const int ki = lanes_below_ull(mI), kd = lanes_below_ull(mD);
-    const bool take = owner < 0 && ki < __popcll(mD);
-    const bool give = owner >= 0 && stk.size() > 0 && kd < __popcll(mI);
-    int e = kTravDone;
-    if (give) stk.pop(e);
-    const int src = take ? select_kth(mD, ki) : lane;
-    const int e_in = coop_bperm(src, e), ow_in = coop_bperm(src, owner);
-    const float tmax_in = coop_bperm(src, wtmax), tmin_in = coop_bperm(src, wtmin);
-    RayInv rin;
-    rin.o = mk3(coop_bperm(src, r.o.x), coop_bperm(src, r.o.y), coop_bperm(src, r.o.z));
-    rin.d = mk3(coop_bperm(src, r.d.x), coop_bperm(src, r.d.y), coop_bperm(src, r.d.z));
-    rin.inv = mk3(coop_bperm(src, r.inv.x), coop_bperm(src, r.inv.y), coop_bperm(src, r.inv.z));
-    rin.oi = mk3(coop_bperm(src, r.oi.x), coop_bperm(src, r.oi.y), coop_bperm(src, r.oi.z));
-    const int nn = coop_bperm(src, r.nx | (r.ny << 8) | (r.nz << 16));
-    if (take) {
-      r = rin;
-      r.nx = nn & 0xff; r.ny = (nn >> 8) & 0xff; r.nz = (nn >> 16) & 0xff;
-      wtmin = tmin_in;
-      wtmax = tmax_in;
-      whit = false;
-      owner = ow_in;
-      stk.clear();
-      if (e_in >= 0) { ref = e_in; pend = 0; }
-      else { pend = e_in; ref = kTravDone; }
-    }
-  }
-  return mine;
-#endif
-}
-
 // Shading record of a closest hit: interpolated normal (triangle.cpp:80-82) or sphere normal
 // (sphere.cpp:78-81), and the material.
 template <int LM = 0>
@@ -1688,7 +1448,24 @@ struct Paths {
   float l1_dir_pdf;
   f3 l1_d;           // the light walk's first direction and its pdf (read back when it starts)
   float l1_pdf;
+#ifdef BDPT_BOUND_WB2
+  VtxS W2[2 * MAXV + 1];   // bound experiment (timing only): a second copy of every stored vertex
+#endif
 };
+#ifdef BDPT_BOUND_WB2
+// the copy is written with volatile stores so that the compiler keeps them although nothing reads it
+template <bool EXT, int MAXV>
+BDPT_HD void vtx_store_dup(Paths<MAXV>& P, const VtxS* slot, const Vtx& v) {
+  VtxS t;
+  vtx_store<EXT>(t, v);
+  volatile uint32_t* d = (volatile uint32_t*)&P.W2[slot - P.E];
+  const uint32_t* q = (const uint32_t*)&t;
+  for (int k = 0; k < (EXT ? 13 : 12); k++) d[k] = q[k];
+}
+#define BDPT_WB2_DUP(P, slot, v) vtx_store_dup<EXT>(P, slot, v)
+#else
+#define BDPT_WB2_DUP(P, slot, v) do {} while (0)
+#endif
 
 struct SampleParams {
   int W, H, spp, max_depth;
@@ -2037,6 +1814,7 @@ BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>&
     v1.gp = 0; v1.cq = 0;
     v1.fwd = mis_p;   // light_constants' L[1] value (set here for the fused walk)
     vtx_store<EXT>(P.L[0], v1);
+    BDPT_WB2_DUP(P, &P.L[0], v1);
     P.l1_dir_pdf = mis_dir;
   };
   Rng gl0 = g;
@@ -2111,6 +1889,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       }
       v.gp = 0.0f;
       em |= DeltaMask<MAXV>(1) << i;   // an s = 0 source (vertex index i = count + 2)
+      BDPT_WB2_DUP(P, &P.E[count], v);
       vtx_store<EXT>(P.E[count++], v);
     }
     if (!end) {
@@ -2179,6 +1958,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
       };
       if (!EXT) finish(1.0f);
       vtx_store<EXT>(*slot, v);
+      BDPT_WB2_DUP(P, slot, v);
       if (i >= sp.max_depth + 1 || count >= MAXV) {
         end = true;
         if (EXT) {
@@ -2266,7 +2046,6 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   while (!walk_step<MAXV, LM, EXT>(S, sp, P, cnt, g, w)) {
   }
 }
-
 // What estimate_bidirection_radiance (bidirection.cpp:296-469) computes for pair (i, j) up to its
 // visibility test: either nothing (zero contribution), a direct eye-image value (s = 0, no ray),
 // or a connection ray on [EPS_F, tmax] whose value (MIS-weighted) counts if it is unoccluded.

@@ -24,6 +24,7 @@ import bdpt_amd as B  # noqa: E402
 CS = os.path.join(REPO, "bidirectional-pathtracing_amd", "csrc")
 DUMP = os.path.join(REPO, "tools", "bin", "libcore_dump_closest.so")
 PROBE = os.path.join(REPO, "tools", "bin", "libclosest_probe.so")
+PROBE_PH = os.path.join(REPO, "tools", "bin", "libclosest_probe_ph.so")   # + lane-use profile
 RAYS = os.path.join(REPO, "tools", "bin", "closest_rays.npy")
 RAYS_ANY = os.path.join(REPO, "tools", "bin", "anyhit_rays.npy")
 
@@ -35,10 +36,11 @@ def build(probe=True):
                     os.path.join(REPO, "tests", "native", "core_cpu.cpp"), os.path.join(CS, "bdpt_scene.cpp")],
                    check=True)
     if probe:
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-slp-vectorize",
-                        "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(REPO, "include"), "-I" + CS,
-                        os.path.join(REPO, "tools", "closest_probe.hip"), os.path.join(CS, "bdpt_scene.cpp"),
-                        "-o", PROBE], check=True)
+        for out, extra in ((PROBE, []), (PROBE_PH, ["-DBDPT_PHASE_PROF"])):
+            subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fno-slp-vectorize",
+                            "-std=c++17", "-shared", "-fPIC", "-I" + os.path.join(REPO, "include"), "-I" + CS,
+                            os.path.join(REPO, "tools", "closest_probe.hip"), os.path.join(CS, "bdpt_scene.cpp"),
+                            "-o", out] + extra + [a for a in sys.argv if a.startswith("-D")], check=True)
 
 
 def dump(sc, W, H, npix, kind=2):
@@ -77,12 +79,15 @@ def main():
     if "--build-only" in sys.argv:
         build()
         return
-    pr = C.CDLL(PROBE)
+    ph = "--phases" in sys.argv
+    pr = C.CDLL(PROBE_PH if ph else PROBE)
     pr.probe_closest.argtypes = [C.POINTER(B.SceneDesc), C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                  C.POINTER(C.c_ulonglong)]
+    pr.probe_cfg_name.restype = C.c_char_p
     d = sc.desc()
-    for any_hit, lm in ((0, 2), (1, 2), (0, 0), (1, 0)):
+    cfgs = [int(x) for x in os.environ.get("PROBE_CFGS", "0,1,2,3,4,5,6").split(",")]
+    for any_hit, lm in ((0, 2), (1, 2)):
         rays = np.load(RAYS_ANY if any_hit else RAYS)
         reps = max(1, (4 << 20) // len(rays))
         base = np.tile(rays, (reps, 1))
@@ -91,23 +96,30 @@ def main():
         for name, rr in orders.items():
             rr = np.ascontiguousarray(rr)
             outs = []
-            for coop in (0, 1):
-                ms, ntop, nodes = C.c_float(), C.c_int(), C.c_ulonglong()
+            for coop in cfgs:
+                ms, ntop, nodes9 = C.c_float(), C.c_int(), (C.c_ulonglong * 9)()
                 out = np.empty((len(rr), 2), np.int32)
                 rc = pr.probe_closest(C.byref(d), rr.ctypes.data_as(C.POINTER(C.c_float)), len(rr), lm, coop, any_hit, 5,
                                       C.byref(ms), C.byref(ntop), out.ctypes.data_as(C.POINTER(C.c_int)),
-                                      C.byref(nodes))
+                                      nodes9)
                 assert rc == 0
+                nodes = nodes9[0]
                 outs.append(out)
+                lp = list(nodes9)[1:]
+                k = 2 if any_hit else 0   # LP_ANODE / LP_CNODE, then the primitive tests
+                prof = (f"; node loop {lp[2 * k] / len(rr) * 64:.2f} wave-iterations per 64 rays at "
+                        f"{lp[2 * k + 1] / max(1, 64 * lp[2 * k]):.1%} lane use, prim tests "
+                        f"{lp[2 * k + 2] / len(rr) * 64:.2f} at {lp[2 * k + 3] / max(1, 64 * lp[2 * k + 2]):.1%}") if ph else ""
                 print(f"{'any    ' if any_hit else 'closest'} LM {lm} treelet {ntop.value:4d} {name:9s} "
-                      f"{'coop ' if coop else 'plain'}: "
+                      f"{pr.probe_cfg_name(coop).decode():11s}: "
                       f"{ms.value:7.3f} ms for {len(rr)} rays = {len(rr) / ms.value / 1e6:6.2f} Grays/s, "
-                      f"{nodes.value / len(rr) / 4:.2f} node steps/ray, hits {np.mean(out[:, 1] >= 0):.3f}", flush=True)
-            same = np.array_equal(outs[0], outs[1])
-            print(f"  identical (t bits, key) for every ray: {same}"
-                  + ("" if same else f" ({np.sum(np.any(outs[0] != outs[1], axis=1))} differ)"), flush=True)
-            if not same:
-                sys.exit(1)
+                      f"{nodes / len(rr) / 4:.2f} node steps/ray, hits {np.mean(out[:, 1] >= 0):.3f}{prof}", flush=True)
+            for k in range(1, len(outs)):
+                same = np.array_equal(outs[0], outs[k])
+                if not same:
+                    print(f"  config {cfgs[k]}: {np.sum(np.any(outs[0] != outs[k], axis=1))} rays differ", flush=True)
+                    sys.exit(1)
+            print("  identical (t bits, key) for every ray in every configuration", flush=True)
 
 
 if __name__ == "__main__":
