@@ -1453,18 +1453,26 @@ struct Paths {
 #endif
 };
 #ifdef BDPT_BOUND_WB2
-// the copy is written with volatile stores so that the compiler keeps them although nothing reads it
+// the copy is written with ordinary (vector) stores; one dword of it at an index the compiler cannot
+// see is read back per sample (BDPT_WB2_USE), so that none of the stores can be dropped
 template <bool EXT, int MAXV>
 BDPT_HD void vtx_store_dup(Paths<MAXV>& P, const VtxS* slot, const Vtx& v) {
-  VtxS t;
-  vtx_store<EXT>(t, v);
-  volatile uint32_t* d = (volatile uint32_t*)&P.W2[slot - P.E];
-  const uint32_t* q = (const uint32_t*)&t;
-  for (int k = 0; k < (EXT ? 13 : 12); k++) d[k] = q[k];
+  vtx_store<EXT>(P.W2[slot - P.E], v);
+}
+template <int MAXV>
+BDPT_HD void wb2_use(const Paths<MAXV>& P) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int k;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(k));
+  const float x = P.W2[k].fwd;
+  asm volatile("; wb2 use %0" ::"v"(x));
+#endif
 }
 #define BDPT_WB2_DUP(P, slot, v) vtx_store_dup<EXT>(P, slot, v)
+#define BDPT_WB2_USE(P) wb2_use(P)
 #else
 #define BDPT_WB2_DUP(P, slot, v) do {} while (0)
+#define BDPT_WB2_USE(P) do {} while (0)
 #endif
 
 struct SampleParams {
@@ -2045,6 +2053,7 @@ BDPT_HD void prepare_sample(const SceneView& S, const SampleParams& sp, Paths<MA
   walk_begin<MAXV, EXT>(S, sp, P, cnt, g, w, x, y, sample);
   while (!walk_step<MAXV, LM, EXT>(S, sp, P, cnt, g, w)) {
   }
+  BDPT_WB2_USE(P);
 }
 // What estimate_bidirection_radiance (bidirection.cpp:296-469) computes for pair (i, j) up to its
 // visibility test: either nothing (zero contribution), a direct eye-image value (s = 0, no ray),

@@ -63,7 +63,7 @@ constexpr int kTopNodes = 1024;
 // flat-list and all-in-LDS scenes stay unsplit). kSbvhAlpha 0 = off. Run-time A/B: BDPT_SBVH=alpha,
 // BDPT_SBVH_BUDGET=fraction.
 constexpr int kSbvhMinPrims = 256;
-constexpr double kSbvhAlpha = 0.0;
+constexpr double kSbvhAlpha = 1e-5;
 constexpr double kSbvhBudget = 0.3;
 
 // LM 3's flat list as one run of primitives: when the device tree's leaves, in DFS order, hold

@@ -270,7 +270,10 @@ static int trace_check_lm(const HostScene& hs, int n, uint64_t seed, int* hits) 
       if (ok && (t < bt || key > bk)) { bt = t; bp = i; bk = key; }
     }
     if (bp >= 0) (*hits)++;
-    if (bp != h.prim || (bp >= 0 && bt != h.t)) bad++;
+    // compared as scene primitives: a primitive that spatial splits reference from two leaves has a
+    // record at two positions, and either may be the one a walk or the loop meets first
+    const int sp = bp >= 0 ? hs.prim_ref[bp] : -1, hp = h.prim >= 0 ? hs.prim_ref[h.prim] : -1;
+    if (sp != hp || (bp >= 0 && bt != h.t)) bad++;
   }
   return bad;
 }
