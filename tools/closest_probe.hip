@@ -306,6 +306,98 @@ BDPT_HD bool trace_any_coop(const SceneView& S, f3 o, f3 d, float tmin, float tm
 #endif
 }
 
+
+// Two queries per lane in one traversal loop (round 6 probe): a lane traces its ray A, then at once
+// its ray B, without waiting for the wave between them, so the wave iterates max over lanes of
+// (steps A + steps B) instead of max(steps A) + max(steps B). This is what tracing a lane's eye and
+// light walk rays together would buy.
+template <int LM = 0, int K = 0, bool ANY = false>
+__device__ void trace_dual(const SceneView& S, const float* ra, const float* rb, bool has_a, bool has_b, Hit& ha,
+                           Hit& hb, Counters& c) {
+  RayInv r;
+  float wtmin = 0;
+  Hit w;
+  w.t = 0; w.prim = -1; w.key = -1; w.b1 = 0; w.b2 = 0;
+  ha = w; hb = w;
+  int stack_mem[kStackMax];
+  TravStack<K> stk(stack_mem, LM == 2 ? lane_stack(S) : nullptr);
+  int ref = kTravDone, pend = 0, phase = 2;
+  auto start = [&](const float* q, int ph) {
+    r = make_rayinv(mk3(q[0], q[1], q[2]), mk3(q[3], q[4], q[5]));
+    wtmin = q[6];
+    w.t = q[7]; w.prim = -1; w.key = -1; w.b1 = 0; w.b2 = 0;
+    stk.clear();
+    ref = S.root;
+    pend = 0;
+    phase = ph;
+    if (ANY) c.shadow++;
+    else c.closest++;
+  };
+  if (has_a) start(ra, 0);
+  else if (has_b) start(rb, 1);
+  float4 a0, a1, a2;
+  bool found = false;   // any hit: the current ray is occluded
+  auto test_leaf = [&](int lf) -> bool {
+    const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
+    a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
+    for (int k = 0; k < cnt; k++) {
+      BDPT_LANE_PROF(c, ANY ? LP_APRIM : LP_CPRIM);
+      const int pi = st + k;
+      float t, b1 = 0, b2 = 0;
+      bool ok;
+      int key;
+      const float4 g0 = a0, g1 = a1, g2 = a2;
+      const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
+      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+      if ((sm >> k) & 1) {
+        c.sphs++;
+        ok = sph_test(g0, r.o, r.d, wtmin, w.t, &t);
+        key = __float_as_int(g1.x);
+      } else {
+        c.tris++;
+        ok = tri_test(g0, g1, g2, r.o, r.d, wtmin, w.t, &t, &b1, &b2);
+        key = __float_as_int(g2.y);
+      }
+      if (ANY && ok) return true;
+      if (ok && (t < w.t || key > w.key)) {
+        w.t = t; w.prim = pi; w.key = key; w.b1 = b1; w.b2 = b2;
+      }
+    }
+    return false;
+  };
+  for (;;) {
+    while (ref >= 0) {
+      BDPT_LANE_PROF(c, ANY ? LP_ANODE : LP_CNODE);
+      ref = node_step<K, LM, ANY ? kAnyOrd : kClosestOrd>(S, r, ref, wtmin, w.t, stk, c);
+      if (ref < 0 && ref != kTravDone && pend == 0) {
+        pend = ref;
+        if (!stk.pop(ref)) ref = kTravDone;
+      }
+      if (wave_count(pend == 0 && ref >= 0) == 0) break;
+    }
+    while (pend != 0) {
+      if (test_leaf(pend)) { found = true; ref = kTravDone; pend = 0; break; }
+      pend = 0;
+      if (ref < 0 && ref != kTravDone) {
+        pend = ref;
+        if (!stk.pop(ref)) ref = kTravDone;
+      }
+    }
+    if (phase < 2 && ref == kTravDone) {   // this ray is done: record it, start the other
+      if (ANY) w.prim = found ? 1 : -1;
+      found = false;
+      if (phase == 0) {
+        ha = w;
+        if (has_b) start(rb, 1);
+        else phase = 2;
+      } else {
+        hb = w;
+        phase = 2;
+      }
+    }
+    if (wave_count(phase < 2) == 0) break;
+  }
+}
 }  // namespace bdpt
 
 constexpr int kProbeBlock = 1024;   // = kLdsStackStride: the LDS stack slots' lane stride
@@ -320,7 +412,7 @@ template <> struct CoopCfg<4> { static constexpr int T = 48; static constexpr bo
 template <> struct CoopCfg<5> { static constexpr int T = 64; static constexpr bool BOT = true; static constexpr int P = 4; };
 template <> struct CoopCfg<6> { static constexpr int T = 32; static constexpr bool BOT = false; static constexpr int P = 4; };
 constexpr const char* kCfgName[] = {"plain", "t16 top x1", "t16 bot x2", "t32 bot x2", "t48 bot x4", "t64 bot x4",
-                                     "t32 top x4"};
+                                     "t32 top x4", "dual (2/lane)"};
 
 template <int LM, int COOP, bool ANY>
 __global__ __launch_bounds__(kProbeBlock, 4) void k_probe_closest(SceneView S, const float* rays, int n, int2* out,
@@ -339,30 +431,49 @@ __global__ __launch_bounds__(kProbeBlock, 4) void k_probe_closest(SceneView S, c
   const long long stride = (long long)gridDim.x * blockDim.x;
   // wave-uniform loop: the wave runs while any of its lanes has a ray left
   const long long wave0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x, wb = wave0; wb < n; i += stride, wb += stride) {
-    const bool have = i < n;
-    const float* r = rays + 8 * (have ? i : 0);
-    Hit h;
-    h.t = 0; h.key = -1;
-    bool ok;
-    if constexpr (ANY) {
-      const f3 o = mk3(r[0], r[1], r[2]), d = mk3(r[3], r[4], r[5]);
-      if constexpr (COOP > 0) {
-        using Q = CoopCfg<COOP>;
-        ok = trace_any_coop<LM, kConnStack, Q::T, Q::BOT, Q::P>(S, o, d, r[6], r[7], c, have);
+  if constexpr (COOP == 7) {
+    // ray pairs (2 j, 2 j + 1) per lane, one traversal loop for both
+    const long long np = (n + 1) / 2;
+    for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x, wb = wave0; wb < np; j += stride, wb += stride) {
+      const long long ia = 2 * j, ib = 2 * j + 1;
+      const bool ha_ = ia < n, hb_ = ib < n;
+      Hit h1, h2;
+      trace_dual<LM, ANY ? kConnStack : kWalkStack, ANY>(S, rays + 8 * (ha_ ? ia : 0), rays + 8 * (hb_ ? ib : 0), ha_, hb_, h1,
+                                                          h2, c);
+      if (ANY) {
+        if (ha_) out[ia] = make_int2(0, h1.prim >= 0 ? 1 : -1);
+        if (hb_) out[ib] = make_int2(0, h2.prim >= 0 ? 1 : -1);
       } else {
-        ok = have && trace_any<LM, kConnStack>(S, o, d, r[6], r[7], c);
+        if (ha_) out[ia] = h1.prim >= 0 ? make_int2(__float_as_int(h1.t), h1.key) : make_int2(0, -1);
+        if (hb_) out[ib] = h2.prim >= 0 ? make_int2(__float_as_int(h2.t), h2.key) : make_int2(0, -1);
       }
-      h.key = ok ? 1 : -1;
-    } else if constexpr (COOP > 0) {
-      using Q = CoopCfg<COOP>;
-      ok = trace_closest_coop<LM, kWalkStack, Q::T, Q::BOT, Q::P>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6],
-                                                                  r[7], h, c, have);
-    } else {
-      ok = false;
-      if (have) ok = trace_closest<LM, kWalkStack>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6], r[7], h, c);
     }
-    if (have) out[i] = ok ? make_int2(__float_as_int(h.t), h.key) : make_int2(0, -1);
+  } else {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x, wb = wave0; wb < n; i += stride, wb += stride) {
+      const bool have = i < n;
+      const float* r = rays + 8 * (have ? i : 0);
+      Hit h;
+      h.t = 0; h.key = -1;
+      bool ok;
+      if constexpr (ANY) {
+        const f3 o = mk3(r[0], r[1], r[2]), d = mk3(r[3], r[4], r[5]);
+        if constexpr (COOP > 0) {
+          using Q = CoopCfg<COOP>;
+          ok = trace_any_coop<LM, kConnStack, Q::T, Q::BOT, Q::P>(S, o, d, r[6], r[7], c, have);
+        } else {
+          ok = have && trace_any<LM, kConnStack>(S, o, d, r[6], r[7], c);
+        }
+        h.key = ok ? 1 : -1;
+      } else if constexpr (COOP > 0 && COOP < 7) {
+        using Q = CoopCfg<COOP>;
+        ok = trace_closest_coop<LM, kWalkStack, Q::T, Q::BOT, Q::P>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6],
+                                                                    r[7], h, c, have);
+      } else {
+        ok = false;
+        if (have) ok = trace_closest<LM, kWalkStack>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6], r[7], h, c);
+      }
+      if (have) out[i] = ok ? make_int2(__float_as_int(h.t), h.key) : make_int2(0, -1);
+    }
   }
   atomicAdd(steps, (unsigned long long)c.nodes);
 #ifdef BDPT_PHASE_PROF
@@ -426,7 +537,7 @@ static int run(const HostScene& hs, const float* d_rays, int n, int2* d_out, int
   return 0;
 }
 
-extern "C" const char* probe_cfg_name(int k) { return k >= 0 && k <= 6 ? kCfgName[k] : "?"; }
+extern "C" const char* probe_cfg_name(int k) { return k >= 0 && k <= 7 ? kCfgName[k] : "?"; }
 
 // lm 0 / 2, coop 0 (plain) / 1..6 (CoopCfg), any 0 (closest hit) / 1 (any hit); out = n x (t bits, reference key) (key -1 =
 // no hit; any hit: key 1 = occluded); ms = mean kernel time
@@ -445,7 +556,7 @@ extern "C" int probe_closest(const bdpt_scene_desc* d, const float* rays, int n,
 #define RUNC(C, A) (lm == 2 ? RUN(2, C, A) : RUN(0, C, A))
 #define RUNA(A)                                                                                       \
   (coop == 0 ? RUNC(0, A) : coop == 1 ? RUNC(1, A) : coop == 2 ? RUNC(2, A) : coop == 3 ? RUNC(3, A)   \
-   : coop == 4 ? RUNC(4, A) : coop == 5 ? RUNC(5, A) : RUNC(6, A))
+   : coop == 4 ? RUNC(4, A) : coop == 5 ? RUNC(5, A) : coop == 6 ? RUNC(6, A) : RUNC(7, A))
   rc = any ? RUNA(true) : RUNA(false);
 #undef RUNA
 #undef RUNC
