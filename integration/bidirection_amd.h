@@ -44,6 +44,15 @@
 // compile check in tests/test_integration.py builds it with the same read access the oracle's
 // ref_driver uses.
 //
+// Several GPUs: BDPT_DEVICES=0,1,... (environment, read by attach) gives the binding one context per
+// listed device. Queued tile batches go to whichever context is free, so up to N batches render at
+// once; every context renders whole pixels (all ns_aa samples) of its tiles, and since the t = 1
+// splats land anywhere the frame is the sum of the contexts' frames: finish() reduces them into the
+// first context's with the C-ABI's RCCL reduce (bdpt_reduce_frames) before it reads the image. The
+// per-tile copy into sampleBuffer reads the launching context's pixels (their splats from other
+// contexts arrive with finish(), as later tiles' splats do on one device). A cell render (set_cell,
+// or lone pixels) uses the first context only. A device listed twice shares its GPU (tests).
+//
 // Threading: the reference's worker threads call raytrace_pixel concurrently (on disjoint tiles).
 // The per-pixel "queued" flags are allocated while the renderer is single-threaded
 // (set_frame_size); the queue, the counters and every bdpt_* call on the context are under one
@@ -57,6 +66,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -153,9 +163,37 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     p.spp = (int32_t)ns_aa;
     p.max_depth = (int32_t)max_ray_depth;
     p.seed = seed;
-    if (ctx_) { bdpt_destroy(ctx_); ctx_ = nullptr; }
-    return bdpt_create(&desc, &p, &ctx_);
+    release();
+    for (int dev : devices()) {   // one context per BDPT_DEVICES entry (default: device 0)
+      p.device = dev;
+      void* c = nullptr;
+      const int rc = bdpt_create(&desc, &p, &c);
+      if (rc != BDPT_OK) { release(); return rc; }
+      ctxs_.push_back(c);
+    }
+    ctx_ = ctxs_[0];
+    busy_.assign(ctxs_.size(), 0);
+    if (ctxs_.size() > 1) {   // the frame is the sum of the contexts' frames (finish)
+      const int rc = bdpt_reduce_create(ctxs_.data(), (int32_t)ctxs_.size(), &red_);
+      if (rc != BDPT_OK) { release(); return rc; }
+    }
+    return BDPT_OK;
   }
+  // the devices of BDPT_DEVICES ("0,1,..."; default {0})
+  static std::vector<int> devices() {
+    std::vector<int> d;
+    const char* e = std::getenv("BDPT_DEVICES");
+    for (const char* q = e; q && *q;) {
+      char* end = nullptr;
+      const long v = std::strtol(q, &end, 10);
+      if (end == q) break;
+      d.push_back((int)v);
+      q = *end == ',' ? end + 1 : end;
+    }
+    if (d.empty()) d.push_back(0);
+    return d;
+  }
+  size_t contexts() { std::lock_guard<std::mutex> lk(mu_); return ctxs_.size(); }
 
   // ---- the PathTracer contract, driven by the reference's unmodified RaytracedRenderer ----
   // start_raytracing calls clear() and then set_frame_size() before it starts the workers
@@ -186,7 +224,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
         cv_.wait(lk, [&] { return copied_ >= mine || failed_.load(); });
       if (queued_ == W * H && !finished_ && !failed_.load()) {
         // the frame's last pixel: wait for the batch in flight, then take the whole frame
-        cv_.wait(lk, [&] { return !launching_ || failed_.load(); });
+        cv_.wait(lk, [&] { return (nbusy_ == 0 && pending_.empty()) || failed_.load(); });
         if (!failed_.load() && !finished_) {
           finished_ = true;
           finish();   // every splat is in (bidirection.cpp:457-466): sampleBuffer <- the image
@@ -248,6 +286,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       th = std::min(kTile, H - y);
       wait = false;
     }
+    if (wait) single_ = true;   // a cell or lone pixels: the first context only (its copies are whole)
     for (size_t yy = y0; yy < y0 + th; yy++)
       for (size_t xx = x0; xx < x0 + tw; xx++) {
         sampleCountBuffer[xx + yy * W] = ns_aa;   // bidirection.cpp:539
@@ -266,9 +305,15 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // (who return at once) go out together in the next bdpt_render. mu_ held on entry and exit,
   // released while the device works.
   void pump(std::unique_lock<std::mutex>& lk) {
-    if (launching_) return;
-    launching_ = true;
     while (!pending_.empty() && !failed_.load()) {
+      // a free context (the first only in a cell render): its launcher goes on while tiles are queued
+      int k = -1;
+      for (size_t c = 0; c < (single_ ? 1 : ctxs_.size()); c++)
+        if (!busy_[c]) { k = (int)c; break; }
+      if (k < 0) return;   // every context busy: their launchers take what is queued
+      busy_[k] = 1;
+      nbusy_++;
+      void* ctx = ctxs_[k];
       std::vector<bdpt_tile> batch;
       batch.swap(pending_);
       const size_t upto = seq_;
@@ -281,9 +326,9 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       const auto t0 = std::chrono::steady_clock::now();
       int rc = BDPT_E_INVALID;
       std::string what;
-      try {   // nothing may leave this section with mu_ released (and launching_ still set)
-        rc = bdpt_render(ctx_, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
-        if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx_) : copy_back(batch, lone, box);   // waits for the launch
+      try {   // nothing may leave this section with mu_ released (and the context still busy)
+        rc = bdpt_render(ctx, batch.data(), (int32_t)batch.size(), 0, (int32_t)ns_aa);
+        if (rc == BDPT_OK) rc = last ? bdpt_sync(ctx) : copy_back(ctx, batch, lone, box);   // waits for the launch
         if (rc != BDPT_OK) what = bdpt_last_error();
       } catch (const std::exception& e) {
         what = e.what();
@@ -291,13 +336,14 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       }
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       lk.lock();
+      busy_[k] = 0;
+      nbusy_--;
       launches_++;
       busy_s_ += dt;
-      copied_ = upto;
+      copied_ = std::max(copied_, upto);
       if (rc != BDPT_OK) record_failure_locked(what);
       cv_.notify_all();
     }
-    launching_ = false;
     cv_.notify_all();
   }
 
@@ -307,8 +353,8 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // queued, and the copy would only delay the next launch. A batch with lone pixels (their
   // callers wait for them, the -p cell path without set_cell) refreshes every queued pixel, read
   // as one rectangle: `box`, the bounding box of what the frame has queued.
-  int copy_back(const std::vector<bdpt_tile>& batch, bool lone, const bdpt_tile& box) {
-    if (batch.size() > 16 && !lone) return bdpt_sync(ctx_);
+  int copy_back(void* ctx, const std::vector<bdpt_tile>& batch, bool lone, const bdpt_tile& box) {
+    if (batch.size() > 16 && !lone) return bdpt_sync(ctx);
     const size_t W = sampleBuffer.w;
     std::vector<float> rgb;
     if (lone) {
@@ -316,7 +362,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
       // all pixels queued so far, so the splats of later samples (bidirection.cpp:457-466) reach
       // the cell's earlier pixels too, and the cell's last batch leaves it complete.
       rgb.resize((size_t)box.w * box.h * 3);
-      int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, box.x0, box.y0, box.w, box.h, rgb.data());
+      int rc = bdpt_read_frame_rect(ctx, BDPT_FRAME_SAMPLE, box.x0, box.y0, box.w, box.h, rgb.data());
       if (rc != BDPT_OK) return rc;
       for (int32_t yy = 0; yy < box.h; yy++)
         for (int32_t xx = 0; xx < box.w; xx++) {
@@ -328,7 +374,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     }
     for (const bdpt_tile& t : batch) {
       rgb.resize((size_t)t.w * t.h * 3);
-      int rc = bdpt_read_frame_rect(ctx_, BDPT_FRAME_SAMPLE, t.x0, t.y0, t.w, t.h, rgb.data());
+      int rc = bdpt_read_frame_rect(ctx, BDPT_FRAME_SAMPLE, t.x0, t.y0, t.w, t.h, rgb.data());
       if (rc != BDPT_OK) return rc;
       for (int32_t yy = 0; yy < t.h; yy++)
         for (int32_t xx = 0; xx < t.w; xx++) {
@@ -400,6 +446,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // Vector3D) is split over up to 16 host threads: 1080p is 6 M vectors.
   void finish() {
     const size_t n = sampleBuffer.w * sampleBuffer.h;
+    if (red_) check(bdpt_reduce_frames(red_, 0));   // every context's frame into the first's
     std::vector<float> eye(n * 3), light(n * 3);
     check(bdpt_read_frame(ctx_, BDPT_FRAME_EYE, eye.data()));
     check(bdpt_read_frame(ctx_, BDPT_FRAME_LIGHT, light.data()));
@@ -421,11 +468,16 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     convert(0, n / nt);
     for (std::thread& x : th) x.join();
   }
-  ~BidirectionalPathTracerAMD() {
-    if (ctx_) bdpt_destroy(ctx_);
-  }
+  ~BidirectionalPathTracerAMD() { release(); }
 
  private:
+  // the reduce before the contexts it reads (bdpt_reduce_destroy), then the contexts
+  void release() {
+    if (red_) { bdpt_reduce_destroy(red_); red_ = nullptr; }
+    for (void* c : ctxs_) bdpt_destroy(c);
+    ctxs_.clear();
+    ctx_ = nullptr;
+  }
   static void copy3(double* d, const Vector3D& v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
   static void check(int rc) {
     if (rc != BDPT_OK) throw std::runtime_error(bdpt_last_error());
@@ -454,7 +506,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   // thread with no worker running (set_frame_size / clear, :280-281).
   void drop_frame() {
     std::lock_guard<std::mutex> lk(mu_);
-    if (ctx_) { bdpt_destroy(ctx_); ctx_ = nullptr; }
+    release();
     const size_t n = sampleBuffer.w * sampleBuffer.h;
     done_.reset(n ? new std::atomic<uint8_t>[n]() : nullptr);   // value-initialised: all 0
     pending_.clear();
@@ -462,7 +514,9 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
     qx1_ = qy1_ = 0;
     queued_ = seq_ = copied_ = launches_ = 0;
     busy_s_ = 0.0;
-    launching_ = finished_ = false;
+    nbusy_ = 0;
+    busy_.assign(busy_.size(), 0);
+    single_ = finished_ = false;
     failed_.store(false);
     err_.clear();
   }
@@ -482,7 +536,12 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   }
 
   static constexpr size_t kTile = 32;   // RaytracedRenderer::imageTileSize (raytraced_renderer.cpp:83)
-  void* ctx_ = nullptr;
+  void* ctx_ = nullptr;                            // the first context (ctxs_[0])
+  std::vector<void*> ctxs_;                        // one per BDPT_DEVICES entry
+  bdpt_reducer* red_ = nullptr;                    // their frame reduce (more than one context)
+  std::vector<char> busy_;                         // per context: a launcher is using it
+  int nbusy_ = 0;
+  bool single_ = false;                            // a cell / lone pixels this frame: first context only
   std::mutex mu_;
   std::condition_variable cv_;
   std::unique_ptr<std::atomic<uint8_t>[]> done_;   // per pixel: queued (with its tile)
@@ -494,7 +553,7 @@ class BidirectionalPathTracerAMD : public BidirectionalPathTracer {
   size_t seq_ = 0, copied_ = 0;                    // tiles queued / tiles whose batch is in sampleBuffer
   size_t launches_ = 0;
   double busy_s_ = 0.0;
-  bool launching_ = false, finished_ = false;
+  bool finished_ = false;
   std::atomic<bool> failed_{false};
   std::string err_;
   std::vector<int32_t> type_, mat_;

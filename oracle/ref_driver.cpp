@@ -463,8 +463,9 @@ int main(int argc, char** argv) {
       return 24;
     }
     fprintf(stdout, "[ref_driver] binding tile loop: %.4f s, %.3f Msamples/s, %zu tiles, %zu bdpt_render "
-            "launches, %.4f s in launches\n", secs, (double)screenW * screenH * ns_aa / secs * 1e-6,
-            amd_pt->tiles_queued(), amd_pt->launches(), amd_pt->device_seconds());
+            "launches, %.4f s in launches, %zu device context(s)\n", secs,
+            (double)screenW * screenH * ns_aa / secs * 1e-6, amd_pt->tiles_queued(), amd_pt->launches(),
+            amd_pt->device_seconds(), amd_pt->contexts());
     if (!npy_prefix.empty()) {
       write_npy(npy_prefix + "_sample.npy", amd_pt->sampleBuffer);
       write_npy(npy_prefix + "_eye.npy", amd_pt->eyeBuffer);
@@ -492,8 +493,9 @@ int main(int argc, char** argv) {
   }
   if (amd_pt)
     fprintf(stdout, "[ref_driver] bdpt_render launches: %zu for %zu tiles; %.4f s in launches of %.4f s in "
-            "render_to_file\n", amd_pt->launches(), amd_pt->tiles_queued(), amd_pt->device_seconds(),
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - loop_t0).count());
+            "render_to_file; %zu device context(s)\n", amd_pt->launches(), amd_pt->tiles_queued(),
+            amd_pt->device_seconds(), std::chrono::duration<double>(std::chrono::steady_clock::now() - loop_t0).count(),
+            amd_pt->contexts());
 #endif
   if (!npy_prefix.empty() && uni) {
     write_npy(npy_prefix + "_sample.npy", rr->pt->sampleBuffer);

@@ -196,3 +196,64 @@ def test_reference_cell_render_through_binding(tmp_path, threads, cell, hook):
     key = f"CBgems_{W}x{H}_s{S}_m{M}_cell_{x0}_{y0}_{dx}_{dy}"
     assert np.array_equal(read_png(str(tmp_path / "cell_rate.png")),
                           read_png(os.path.join(REPO, "tests", "golden", "png", key + "_rate.png")))
+
+
+def _two_ctx_env(devices):
+    return dict(os.environ, BDPT_DEVICES=devices)
+
+
+@needs_bin
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", ["0,0", "0,1"])
+def test_reference_render_loop_on_two_contexts(tmp_path, devices):
+    """BDPT_DEVICES: the binding's contexts on the listed devices ("0,0": two contexts sharing the
+    one GPU of this pool's boxes; "0,1": two GPUs, skipped below 2 devices). The reference's
+    unmodified render_to_file at -t 8 hands tile batches to whichever context is free; finish()
+    sums the contexts' frames with the RCCL reduce before save_image. The PNG must equal the
+    product CLI's one-device render (fp32 splat order aside) and the buffers the oracle's mode 2."""
+    from _util import device_count
+    if devices == "0,1" and device_count() < 2:
+        pytest.skip("needs >= 2 visible GPUs (this pool's boxes have one)")
+    import bdpt_amd as B
+    from test_output_stage import CLI, read_png
+    W, H, S, M = 200, 150, 2, 5
+    prefix = str(tmp_path / "loop")
+    png = str(tmp_path / "loop.png")
+    r = subprocess.run([AMD, "-A", "-t", "8", "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-f", png, "-o", prefix,
+                        os.path.join(REPO, "scenes", "CBspheres.dae")], capture_output=True, text=True, timeout=300,
+                       cwd=tmp_path, env=_two_ctx_env(devices))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "2 device context(s)" in r.stdout, r.stdout
+    ntiles = ((W + 31) // 32) * ((H + 31) // 32)
+    queued = int(r.stdout.split("bdpt_render launches:")[1].split()[2])
+    assert queued == ntiles
+    sc = B.load_dae(os.path.join(REPO, "scenes", "CBspheres.dae"), W, H)
+    samp, eye, light, _ = oracle_render(sc, W, H, S, M, MODE_C32)
+    for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
+        assert float(np.sqrt(np.mean((np.load(f"{prefix}_{name}.npy") - ref) ** 2))) < 1e-4, name
+    cli_png = tmp_path / "cli.png"
+    rc = subprocess.run([CLI, "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-f", str(cli_png), "--no-stats",
+                         os.path.join(REPO, "scenes", "CBspheres.dae")], capture_output=True, text=True, timeout=300)
+    assert rc.returncode == 0, rc.stderr
+    d = np.abs(read_png(png).astype(int) - read_png(cli_png).astype(int))
+    print(f"two contexts ({devices}): PNG bytes differing {np.count_nonzero(d)} of {d.size}, max {d.max()}")
+    assert d.max() <= 1 and np.count_nonzero(d) <= 0.001 * d.size
+
+
+@needs_bin
+@pytest.mark.gpu
+def test_tile_loop_on_two_contexts(tmp_path):
+    """The reference's worker loop through the binding with BDPT_DEVICES=0,0: batches on both
+    contexts, the summed frame within the parity tolerance of oracle mode 2."""
+    W, H, S, M = 320, 240, 2, 5
+    prefix = str(tmp_path / "tl")
+    r = subprocess.run([AMD, "-B", "-t", "8", "-s", str(S), "-m", str(M), "-r", str(W), str(H), "-o", prefix,
+                        os.path.join(REPO, "scenes", "CBspheres.dae")], capture_output=True, text=True, timeout=300,
+                       cwd=tmp_path, env=_two_ctx_env("0,0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "2 device context(s)" in r.stdout, r.stdout
+    import bdpt_amd as B
+    sc = B.load_dae(os.path.join(REPO, "scenes", "CBspheres.dae"), W, H)
+    samp, eye, light, _ = oracle_render(sc, W, H, S, M, MODE_C32)
+    for name, ref in (("sample", samp), ("eye", eye), ("light", light)):
+        assert float(np.sqrt(np.mean((np.load(f"{prefix}_{name}.npy") - ref) ** 2))) < 1e-4, name
