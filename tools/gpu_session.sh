@@ -1,5 +1,5 @@
 #!/bin/bash
-# The GPU session script (round 5 onward; earlier per-round scripts are in tools/archive/).
+# The GPU session script (round 5 onward; the earlier per-round scripts were removed in round 6, git history has them).
 #   PART=tests    the whole `pytest -m gpu` suite
 #   PART=phases   phase split + lane use per phase (BDPT_PHASE_PROF variants build_var_ph.so (m <= 5)
 #                 and build_var_ph8.so (m <= 8), tools/build_variants.sh) on the north star and C5
@@ -13,7 +13,7 @@
 #   PART=full     tests, then bench
 # Every GPU step runs under its own timeout; the script stops at the first abort / fault / timeout.
 cd "$(dirname "$0")/.." || exit 1
-OUT=gpurun_out/${TAG:-r05}
+OUT=gpurun_out/${TAG:-r06}
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() {  # name, timeout, cmd...
