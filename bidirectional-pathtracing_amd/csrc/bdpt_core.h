@@ -1434,8 +1434,10 @@ BDPT_HD Vtx vtx_load(const VtxS& s) {
 // Per-subpath bit masks indexed by the reference's vertex index k <= MAXV + 1: 32 bits up to the
 // m = 16 kernels (unchanged code), 64 for the m <= 32 and m <= 62 ones.
 template <int MAXV>
-using DeltaMask = typename std::conditional<(MAXV > 29), uint64_t, uint32_t>::type;
+using DeltaMask = typename std::conditional<
+    (MAXV > 62), unsigned __int128, typename std::conditional<(MAXV > 29), uint64_t, uint32_t>::type>::type;
 static_assert(sizeof(DeltaMask<62>) * 8 >= 62 + 2, "delta mask holds vertex indices up to MAXV + 1");
+static_assert(sizeof(DeltaMask<126>) * 8 >= 126 + 2, "delta mask holds vertex indices up to MAXV + 1");
 
 template <int MAXV>
 struct Paths {

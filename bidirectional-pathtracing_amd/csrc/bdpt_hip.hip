@@ -65,6 +65,10 @@ __device__ __forceinline__ int wave_max(int v) {
 }
 __device__ __forceinline__ int ctz_mask(uint32_t m) { return __builtin_ctz(m); }
 __device__ __forceinline__ int ctz_mask(uint64_t m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ int ctz_mask(unsigned __int128 m) {   // the m <= 126 kernels' 128-bit masks
+  const uint64_t lo = (uint64_t)m;
+  return lo ? __builtin_ctzll(lo) : 64 + __builtin_ctzll((uint64_t)(m >> 64));
+}
 // number of set bits of m below this lane (ballot + mbcnt prefix sum)
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -168,7 +172,7 @@ constexpr int kLdsMats = 48, kLdsLights = 8;
 constexpr size_t kLdsStackBytes = (size_t)kLdsStack * kBlock * sizeof(int);   // LM 1 (when it fits) and 2
 
 constexpr size_t kStaticLds = kLdsMats * sizeof(DMat) + kLdsLights * sizeof(DLight);
-constexpr int kMaxDepth = 62;   // the deepest k_bdpt_sample instantiation (MAXV = 62: vertex index <= 63, 64-bit delta masks)
+constexpr int kMaxDepth = 126;   // the deepest k_bdpt_sample instantiation (MAXV = 126: vertex index <= 127, 128-bit delta masks)
 #define BDPT_STR2(x) #x
 #define BDPT_STR(x) BDPT_STR2(x)
 
@@ -753,13 +757,13 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
     g_err = "invalid frame size / spp / max_depth";
     return BDPT_E_INVALID;
   }
-  // the kernels hold a subpath in a fixed array: instantiations for m <= 5, 8, 16, 32 and 62 (the
-  // reference's vectors have no cap, bidirection.cpp:84-86; deeper paths are rejected cleanly: a
-  // subpath's vertex index must fit the 64-bit delta masks)
+  // the kernels hold a subpath in a fixed array: instantiations for m <= 5, 8, 16, 32, 62 and 126
+  // (the reference's vectors have no cap, bidirection.cpp:84-86; deeper paths are rejected cleanly:
+  // a subpath's vertex index must fit the 128-bit delta masks)
   int need = p.max_depth < 1 ? 1 : p.max_depth;
   if (need > kMaxDepth) {
     g_err = "max_depth " + std::to_string(p.max_depth) + " > " + std::to_string(kMaxDepth) +
-            ": the deepest kernel holds subpaths of up to 62 bounces";
+            ": the deepest kernel holds subpaths of up to 126 bounces";
     return BDPT_E_UNSUPPORTED;
   }
   // 0 = auto = 1: the persistent megakernel. 2 was the wavefront pipeline (per-bounce kernels with
@@ -777,7 +781,7 @@ int bdpt_create(const bdpt_scene_desc* scene, const bdpt_params* params, void** 
   if (p.pipeline < 0 || p.pipeline > 2) { g_err = "bad pipeline (0 = auto, 1 = megakernel)"; return BDPT_E_INVALID; }
   Ctx* c = new Ctx();
   c->prm = p;
-  c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 62;
+  c->maxv = need <= 5 ? 5 : need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : need <= 62 ? 62 : 126;
   // diagnostics / A-B switches, read once per ctx (tests set them before bdpt_create)
   auto env_int = [](const char* name, int dflt) { const char* v = getenv(name); return v ? atoi(v) : dflt; };
   c->env_lds_mode = env_int("BDPT_LDS_MODE", -1);
@@ -1006,7 +1010,7 @@ int bdpt_render(void* ctx, const bdpt_tile* tiles, int32_t ntiles, int32_t spp_b
 #else
   int rc = c->maxv == 5 ? launch_maxv<5>(c, kp) : c->maxv == 8 ? launch_maxv<8>(c, kp)
            : c->maxv == 16 ? launch_maxv<16>(c, kp) : c->maxv == 32 ? launch_maxv<32>(c, kp)
-           : launch_maxv<62>(c, kp);
+           : c->maxv == 62 ? launch_maxv<62>(c, kp) : launch_maxv<126>(c, kp);
 #endif
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->ev1, c->stream));

@@ -90,6 +90,7 @@ static int render_maxv(const HostScene& hs, int W, int H, int spp, int M, uint64
   if (need <= 16) return run<16, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   if (need <= 32) return run<32, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   if (need <= 62) return run<62, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
+  if (need <= 126) return run<126, LM, EXT>(hs, W, H, spp, M, seed, s0, count, pixels, npix, eye, light, stats, rr);
   return BDPT_E_UNSUPPORTED;
 }
 

@@ -124,15 +124,16 @@ def test_dae_missing_file():
 
 
 def test_depth_limits_rejected_before_device():
-    """The kernels hold a subpath in a fixed array: m <= 62 is instantiated (the reference's vectors
-    have no cap, bidirection.cpp:84-86); m = 63 is rejected cleanly with the reason, as is a
-    PathTracer depth past its 21 recorded vertices. m = 62 passes the checks (then needs a device)."""
+    """The kernels hold a subpath in a fixed array: m <= 126 is instantiated (the reference's vectors
+    have no cap, bidirection.cpp:84-86); m = 127 is rejected cleanly with the reason, as is a
+    PathTracer depth past its 21 recorded vertices. m = 126 passes the checks (then needs a device)."""
     sc = golden_scene("CBspheres", 32, 24)
     lib = B.load_library()
     p = B.Params()
     p.width, p.height, p.spp = 32, 24, 1
     ctx = C.c_void_p()
-    for m, pt, unsupported in ((63, False, True), (62, False, False), (22, True, True), (21, True, False)):
+    for m, pt, unsupported in ((127, False, True), (126, False, False), (63, False, False), (22, True, True),
+                               (21, True, False)):
         p.max_depth = m
         p.integrator = B.INTEGRATOR_PT if pt else B.INTEGRATOR_BDPT
         rc = lib.bdpt_create(C.byref(sc.desc()), C.byref(p), C.byref(ctx))

@@ -53,7 +53,9 @@ CASES = [("CBspheres", 32, 24, 2, 5), ("CBspheres_lambertian", 32, 24, 2, 5), ("
          # the m <= 32 and m <= 62 kernels (64-bit delta masks): mirror / glass chains run long here
          ("CBspheres", 24, 18, 2, 20), ("CBgems", 24, 18, 1, 32),
          # the m <= 62 kernel
-         ("CBspheres", 24, 18, 1, 62)]
+         ("CBspheres", 24, 18, 1, 62),
+         # the m <= 126 kernel (128-bit delta masks)
+         ("CBspheres", 16, 12, 1, 100)]
 
 
 @pytest.mark.parametrize("lds_mode", [0, 1, 3])

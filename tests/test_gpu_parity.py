@@ -55,6 +55,7 @@ def _rmse(a, b):
     ("CBspheres", 96, 72, 2, 20),    # the m <= 32 kernel (the reference has no depth cap)
     ("CBgems", 64, 48, 1, 32),
     ("CBspheres", 64, 48, 1, 62),    # the m <= 62 kernel
+    ("CBspheres", 48, 36, 1, 100),   # the m <= 126 kernel (128-bit delta masks)
 ])
 def test_parity_vs_oracle(name, W, H, S, M, pipe):
     sc = golden_scene(name, W, H)
