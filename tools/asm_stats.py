@@ -6,10 +6,11 @@ flags (plus any extra -D flags given on the command line) and prints, per k_bdpt
 instantiation: VGPRs, scratch bytes per lane, code size, instruction count, scratch / VMEM / LDS
 instruction counts and exec-mask bookkeeping. Used to pre-screen A/B variants before a GPU run.
 
-  python3 tools/asm_stats.py [-DFOO=1 ...]
+  python3 tools/asm_stats.py [-DFOO=1 ...]     (ASM_EXTRA="-mllvm ..." adds other compiler flags)
 """
 import os
 import re
+import shlex
 import subprocess
 import sys
 from collections import Counter
@@ -19,8 +20,8 @@ CS = os.environ.get('ASM_CS', os.path.join(ROOT, 'bidirectional-pathtracing_amd'
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
-extra = [a for a in sys.argv[1:] if a.startswith("-D")]
-tag = "_".join(a[2:].replace("=", "") for a in extra) or "default"
+extra = [a for a in sys.argv[1:] if a.startswith("-D")] + shlex.split(os.environ.get("ASM_EXTRA", ""))
+tag = re.sub(r"[^A-Za-z0-9]+", "_", "_".join(extra)).strip("_")[:80] or "default"
 out = f"/tmp/asm_{tag}.s"
 cmd = [ge.HIPCC] + [f for f in ge.HIP_FLAGS if f not in ("-fPIC",)] + [
     "-I" + os.path.join(ROOT, "include"), "-I" + CS, "--cuda-device-only", "-S",
