@@ -284,9 +284,12 @@ struct Counters {
   uint32_t lnodes = 0;   // of `nodes`: child AABBs read from the block's LDS copy (LM 1, LM 2 treelet)
   uint32_t env_s = 0, env_l = 0, env_p = 0;   // environment-light samples / radiance / pdf lookups
 #ifdef BDPT_PHASE_PROF
-  unsigned long long clk_walk_trace = 0;   // cycles in the walk's closest-hit queries (profiling builds)
-  unsigned long long clk_light = 0;        // ... drawing the light vertex L[1] (sample_light_ray)
-  unsigned long long clk_vertex = 0;       // ... from a hit to the next ray (shading record, vertex, sample_f)
+  // wave-level cycles (each interval counted by the wave's lowest active lane, BDPT_WAVE_CLK; the
+  // kernel sums its lanes): in the walk's closest-hit queries, drawing the light vertex L[1]
+  // (sample_light_ray), and from a hit to the next ray (shading record, vertex, sample_f)
+  unsigned long long clk_walk_trace = 0;
+  unsigned long long clk_light = 0;
+  unsigned long long clk_vertex = 0;
   // lane use per phase: [2k] wave-level iterations (counted by the wave's lowest active lane),
   // [2k + 1] active lanes summed over them (every active lane counts itself); k = LP_*
   uint32_t lp[2 * 8] = {};
@@ -310,6 +313,13 @@ enum {
     const unsigned long long m_ = __ballot(1);                                                    \
     if ((unsigned)__lane_id() == (unsigned)__builtin_ctzll(m_)) (c).lp[2 * (k)]++;                \
     (c).lp[2 * (k) + 1]++;                                                                        \
+  } while (0)
+// a wave-level interval of dt cycles (s_memtime is the wave's clock): added once, by the lowest
+// active lane, so that an interval is counted whichever lanes take part in it
+#define BDPT_WAVE_CLK(acc, dt)                                                                    \
+  do {                                                                                            \
+    const unsigned long long m_ = __ballot(1);                                                    \
+    if ((unsigned)__lane_id() == (unsigned)__builtin_ctzll(m_)) (acc) += (dt);                    \
   } while (0)
 #else
 #define BDPT_LANE_PROF(c, k) \
@@ -1835,7 +1845,7 @@ BDPT_HD void walk_begin(const SceneView& S, const SampleParams& sp, Paths<MAXV>&
 #endif
   sample_light(gl0, lo, ld, ln, la1, ldp);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
-  cnt.clk_light += __builtin_amdgcn_s_memtime() - tl0;
+  BDPT_WAVE_CLK(cnt.clk_light, __builtin_amdgcn_s_memtime() - tl0);
 #endif
   w.lpos = gl0.pos;
   P.l1_d = ld;
@@ -1879,7 +1889,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
     bool end = !trace_closest<LM, kWalkStack>(S, ro, rd, rmin, rmax, h, cnt);
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
-    cnt.clk_walk_trace += tq1 - tq0;
+    BDPT_WAVE_CLK(cnt.clk_walk_trace, tq1 - tq0);
 #endif
     if (EXT && end && !light && S.env.light >= 0) {
       // an escaped eye ray ends on the environment light: vertex at infinity in direction rd
@@ -2007,7 +2017,7 @@ BDPT_HD bool walk_step(const SceneView& S, const SampleParams& sp, Paths<MAXV>& 
         if (!nonzero3(nalpha)) end = true;
       }
 #if defined(BDPT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
-      cnt.clk_vertex += __builtin_amdgcn_s_memtime() - tq1;
+      BDPT_WAVE_CLK(cnt.clk_vertex, __builtin_amdgcn_s_memtime() - tq1);
 #endif
     }
     if (end) {

@@ -58,6 +58,11 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -490,15 +495,20 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_bdpt_sample(KParams kp) {
 #endif
   }
 #ifdef BDPT_PHASE_PROF
-  if (lane == 0) {
-    atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
-    atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
-    atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
-    atomicAdd((unsigned long long*)kp.prof + 3, cnt.clk_walk_trace);
-    atomicAdd((unsigned long long*)kp.prof + 4, ph_walk_wave);
-    atomicAdd((unsigned long long*)kp.prof + 6, ph_cells);
-    atomicAdd((unsigned long long*)kp.prof + 8, cnt.clk_light);
-    atomicAdd((unsigned long long*)kp.prof + 9, cnt.clk_vertex);
+  {
+    // the wave-level clocks were added by whichever lane was the lowest active one (BDPT_WAVE_CLK)
+    const unsigned long long ct = wave_sum64(cnt.clk_walk_trace), cl = wave_sum64(cnt.clk_light),
+                             cv = wave_sum64(cnt.clk_vertex);
+    if (lane == 0) {
+      atomicAdd((unsigned long long*)kp.prof + 0, ph_prep);
+      atomicAdd((unsigned long long*)kp.prof + 1, ph_gen - ph_flush);
+      atomicAdd((unsigned long long*)kp.prof + 2, ph_flush);
+      atomicAdd((unsigned long long*)kp.prof + 3, ct);
+      atomicAdd((unsigned long long*)kp.prof + 4, ph_walk_wave);
+      atomicAdd((unsigned long long*)kp.prof + 6, ph_cells);
+      atomicAdd((unsigned long long*)kp.prof + 8, cl);
+      atomicAdd((unsigned long long*)kp.prof + 9, cv);
+    }
   }
 #pragma unroll
   for (int k = 0; k < 16; k++) {   // lane-use profile: prof[16 + k]
