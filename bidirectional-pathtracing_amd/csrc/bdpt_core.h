@@ -641,17 +641,52 @@ BDPT_HD int ld_lds_i(const int* p) {
 }
 // A 4-wide node's rows as the ray sees them: v[0] / v[1] = the x plane rows nearer / farther along
 // the ray (lo.x / hi.x, swapped when the direction's x is negative), v[2] / v[3] y, v[4] / v[5] z,
-// v[6] the child references. Byte offsets within the node: near = 32 a + n_a, far = 32 a + 16 - n_a.
-BDPT_HD void ld_node4_oct_glb(const float4* p, const RayInv& r, float4* v) {
-  const char* b = (const char*)p;
-  const int nx = r.nx, ny = r.ny, nz = r.nz;
-  v[0] = ld_glb4((const float4*)(b + nx));
-  v[1] = ld_glb4((const float4*)(b + 16 - nx));
-  v[2] = ld_glb4((const float4*)(b + 32 + ny));
-  v[3] = ld_glb4((const float4*)(b + 48 - ny));
-  v[4] = ld_glb4((const float4*)(b + 64 + nz));
-  v[5] = ld_glb4((const float4*)(b + 80 - nz));
-  v[6] = ld_glb4((const float4*)(b + 96));
+// v[6] the child references. Byte offsets within node ref: near = 128 ref + 32 a + n_a, far =
+// 128 ref + 32 a + 16 - n_a. The address is the node array's base (wave-uniform: the scalar part of
+// a global load) plus a 32-bit per-lane byte offset, the row's constant part in the immediate field:
+// against a 64-bit address per row (round 6, profiles/r06qrs_ab_lean_node.log) the per-ray offsets
+// take 6 VGPRs instead of 12 and the north-star kernel's static scratch instructions fall 236 -> 187.
+BDPT_HD void ld_node4_oct_glb(const float4* nodes, int ref, const RayInv& r, float4* v) {
+  const char* b = (const char*)nodes;
+  const uint32_t o = (uint32_t)ref * 128u;
+  const uint32_t nx = (uint32_t)r.nx, ny = (uint32_t)r.ny, nz = (uint32_t)r.nz;
+  v[0] = ld_glb4((const float4*)(b + (size_t)(o + nx)));
+  v[1] = ld_glb4((const float4*)(b + (size_t)(o + (16u - nx))));
+  v[2] = ld_glb4((const float4*)(b + 32 + (size_t)(o + ny)));
+  v[3] = ld_glb4((const float4*)(b + 32 + (size_t)(o + (16u - ny))));
+  v[4] = ld_glb4((const float4*)(b + 64 + (size_t)(o + nz)));
+  v[5] = ld_glb4((const float4*)(b + 64 + (size_t)(o + (16u - nz))));
+  v[6] = ld_glb4((const float4*)(b + 96 + (size_t)o));
+}
+// The same as one asm block: the seven loads issue back to back under one wait. LM 0 (every node from
+// HBM) needs it: left to the compiler, its loads were spaced by waits and the reference row (needed
+// only once a child is hit) sank behind the slab tests, a second dependent fetch per step (LM 0
+// 703 -> 647). LM 2's HBM path (waves with a lane below the treelet) runs faster with the compiler's
+// schedule (north star 782 asm vs 792), so it keeps the C++ form.
+BDPT_HD void ld_node4_oct_glb_asm(const float4* nodes, int ref, const RayInv& r, float4* v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const char* b = (const char*)nodes;
+  const uint32_t o = (uint32_t)ref * 128u;
+  const uint32_t nx = (uint32_t)r.nx, ny = (uint32_t)r.ny, nz = (uint32_t)r.nz;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f t[7];
+  asm volatile(
+      "global_load_dwordx4 %0, %7, %14\n\t"
+      "global_load_dwordx4 %1, %8, %14\n\t"
+      "global_load_dwordx4 %2, %9, %14 offset:32\n\t"
+      "global_load_dwordx4 %3, %10, %14 offset:32\n\t"
+      "global_load_dwordx4 %4, %11, %14 offset:64\n\t"
+      "global_load_dwordx4 %5, %12, %14 offset:64\n\t"
+      "global_load_dwordx4 %6, %13, %14 offset:96\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6])
+      : "v"(o + nx), "v"(o + (16u - nx)), "v"(o + ny), "v"(o + (16u - ny)), "v"(o + nz), "v"(o + (16u - nz)),
+        "v"(o), "s"(b));
+#pragma unroll
+  for (int k = 0; k < 7; k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
+#else
+  ld_node4_oct_glb(nodes, ref, r, v);
+#endif
 }
 // the same from the LDS copy
 BDPT_HD void ld_node4_oct_lds(const float4* p, const RayInv& r, float4* v) {
@@ -677,7 +712,7 @@ BDPT_HD void ld_node4_oct_lds(const float4* p, const RayInv& r, float4* v) {
 #pragma unroll
   for (int k = 0; k < 7; k++) v[k] = make_float4(t[k].x, t[k].y, t[k].z, t[k].w);
 #else
-  ld_node4_oct_glb(p, r, v);
+  ld_node4_oct_glb(p, 0, r, v);
 #endif
 }
 
@@ -710,13 +745,13 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
         ld_node4_oct_lds(S.lnodes + node_f4(W) * ref, r, v);
         c.lnodes += W;
       } else {
-        ld_node4_oct_glb(S.nodes + node_f4(W) * ref, r, v);
+        ld_node4_oct_glb(S.nodes, ref, r, v);
       }
     } else if (LM == 1) {
       ld_node4_oct_lds(S.lnodes + node_f4(W) * ref, r, v);
       c.lnodes += W;
     } else {
-      ld_node4_oct_glb(S.nodes + node_f4(W) * ref, r, v);
+      ld_node4_oct_glb_asm(S.nodes, ref, r, v);
     }
   } else if (LM == 1) {   // 2-wide, all nodes in LDS: plain ds_reads the compiler schedules
 #pragma unroll
@@ -765,14 +800,17 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
     TF = fminf(fminf(fmaf(hx.C, r.inv.x, -r.oi.x), fmaf(hy.C, r.inv.y, -r.oi.y)),            \
                fmaf(hz.C, r.inv.z, -r.oi.z)) * 1.00000024f;                                  \
   }
+    // An empty slot (reference kTravDone) holds an inverted infinite box (bdpt_scene.cpp): its near
+    // distance is +inf and its far one -inf, so its test fails without a look at the reference, and
+    // the reference row is needed only once a child is hit (round 6: north star +1.7 % by itself).
     BDPT_SLAB_OCT(x, tn0, tf);
-    h0 = r0 != kTravDone && fmaxf(tn0, tmin) <= fminf(tf, tmax);
+    h0 = fmaxf(tn0, tmin) <= fminf(tf, tmax);
     BDPT_SLAB_OCT(y, tn1, tf);
-    h1 = r1 != kTravDone && fmaxf(tn1, tmin) <= fminf(tf, tmax);
+    h1 = fmaxf(tn1, tmin) <= fminf(tf, tmax);
     BDPT_SLAB_OCT(z, tn2, tf);
-    h2 = r2 != kTravDone && fmaxf(tn2, tmin) <= fminf(tf, tmax);
+    h2 = fmaxf(tn2, tmin) <= fminf(tf, tmax);
     BDPT_SLAB_OCT(w, tn3, tf);
-    h3 = r3 != kTravDone && fmaxf(tn3, tmin) <= fminf(tf, tmax);
+    h3 = fmaxf(tn3, tmin) <= fminf(tf, tmax);
 #undef BDPT_SLAB_OCT
     if (ORD == 0) {
       // continue with the lowest hit slot, push the others

@@ -746,9 +746,11 @@ int build_host_scene(const bdpt_scene_desc* d, HostScene& out, std::string& err,
         N[13] = i2f(ref_of(ch[1]));
       } else {
         // SoA over the children: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] | refs[4] | pad;
-        // an empty slot has ref kTravDone and a zero box (never read)
+        // an empty slot has ref kTravDone and an inverted infinite box (lo +inf, hi -inf): whatever
+        // the direction's signs, its near plane distance is +inf and its far one -inf (no NaN for a
+        // finite inverse), so its slab test fails without looking at the reference
         for (int s = 0; s < W; s++) {
-          float v[6] = {0, 0, 0, 0, 0, 0};
+          float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
           int rf = kTravDone;
           if (s < (int)ch.size()) {
             child_box(ch[s], v);
