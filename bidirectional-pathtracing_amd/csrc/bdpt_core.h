@@ -334,11 +334,16 @@ struct Hit {
   float b1, b2;
 };
 
+// Both predicates with non-short-circuit & / |: each term a lane mask, combined without a branch.
+// Written with && / || (and the early-outs joined by ||), the compiler emitted an exec-mask branch
+// per term — ~40 scalar / vector instructions per check in the leaf loops; flat, the north-star
+// kernel has 650 fewer static instructions and runs +3.3 % (CBspheres +14 %, CBgems m7 +5 %,
+// profiles/r06v_ab_tri_flat.log). Same predicates, same results.
 BDPT_HD bool quot_neg(float n, float d) {
-  return ((n < 0 && d > 0) || (n > 0 && d < 0)) && fabsf(n) >= fabsf(d) * 8.67361738e-19f;  // 2^-60
+  return (((n < 0) & (d > 0)) | ((n > 0) & (d < 0))) & (fabsf(n) >= fabsf(d) * 8.67361738e-19f);  // 2^-60
 }
 BDPT_HD bool quot_gt1(float n, float d) {
-  return ((n > 0 && d > 0) || (n < 0 && d < 0)) && fabsf(n) > fabsf(d);
+  return (((n > 0) & (d > 0)) | ((n < 0) & (d < 0))) & (fabsf(n) > fabsf(d));
 }
 
 // Möller–Trumbore exactly as Triangle::intersect (triangle.cpp:57-95), fp32.
@@ -354,10 +359,10 @@ BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f
   // Exact early-outs before the three correctly-rounded divisions: only when the rounded
   // quotient is certainly < 0 (opposite signs, |q| >= 2^-60 so it cannot round to -0) or > 1
   // (|n| > |denom| implies fl(n/denom) > 1), i.e. exactly when the reference test fails anyway.
-  if (quot_neg(n1, denom) || quot_gt1(n1, denom)) return false;
+  if (quot_neg(n1, denom) | quot_gt1(n1, denom)) return false;
   f3 s2 = cross(s, e1);
   float n2 = dot(s2, d);
-  if (quot_neg(n2, denom) || quot_gt1(n2, denom)) return false;
+  if (quot_neg(n2, denom) | quot_gt1(n2, denom)) return false;
   float nt = dot(s2, e2);
   if (tmin >= 0 && quot_neg(nt, denom)) return false;
   float t = nt / denom;
