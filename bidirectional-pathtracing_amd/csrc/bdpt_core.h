@@ -103,7 +103,7 @@ BDPT_HD f3 to_world(const Frame& f, f3 v) { return add(add(smul(v.x, f.X), smul(
 BDPT_HD float lz(f3 v, f3 Z) { return v.x * Z.x + v.y * Z.y + v.z * Z.z; }   // (w2o*v).z
 BDPT_HD f3 to_local(const Frame& f, f3 v) { return mk3(lz(v, f.X), lz(v, f.Y), lz(v, f.Z)); }
 BDPT_HD f3 zaxis(f3 n) { return normalize(n); }   // make_coord_space(n).Z without X, Y
-BDPT_HD bool nonzero3(f3 v) { return v.x != 0 || v.y != 0 || v.z != 0; }
+BDPT_HD bool nonzero3(f3 v) { return (v.x != 0) | (v.y != 0) | (v.z != 0); }
 
 // ------------------------------------------------------------------------------------------------
 // Counter RNG: Philox4x32-10, counter (pixel, sample, block, 0xB1D1), key (seed lo, hi).
@@ -364,12 +364,12 @@ BDPT_HD bool tri_test(const float4 g0, const float4 g1, const float4 g2, f3 o, f
   float n2 = dot(s2, d);
   if (quot_neg(n2, denom) | quot_gt1(n2, denom)) return false;
   float nt = dot(s2, e2);
-  if (tmin >= 0 && quot_neg(nt, denom)) return false;
+  if ((tmin >= 0) & quot_neg(nt, denom)) return false;
   float t = nt / denom;
   float b1 = n1 / denom;
   float b2 = n2 / denom;
   *t_out = t; *b1_out = b1; *b2_out = b2;
-  return t >= tmin && t <= tmax && b1 >= 0 && b2 >= 0 && b1 + b2 <= 1;
+  return (t >= tmin) & (t <= tmax) & (b1 >= 0) & (b2 >= 0) & (b1 + b2 <= 1);
 }
 
 // Sphere::test + intersect (sphere.cpp:11-35,61-93) with the quadratic in fp64.
@@ -394,9 +394,8 @@ BDPT_HD bool sph_test(const float4 g0, f3 o, f3 d, float tmin, float tmax, float
   double root = sqrt(delta);
   double t1 = (-b - root) / (2 * a);
   double t2 = (-b + root) / (2 * a);
-  double t = -1;
-  if (t1 >= (double)tmin && t1 <= (double)tmax) t = t1;
-  else if (t2 >= (double)tmin && t2 <= (double)tmax) t = t2;
+  const bool in1 = (t1 >= (double)tmin) & (t1 <= (double)tmax), in2 = (t2 >= (double)tmin) & (t2 <= (double)tmax);
+  const double t = in1 ? t1 : in2 ? t2 : -1.0;
   if (t > 0) {
     *t_out = (float)t;
     return true;
@@ -902,7 +901,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
         ok = tri_test(g0, g1, g2, o, d, tmin, h.t, &t, &b1, &b2);
         key = __float_as_int(g2.y);
       }
-      if (ok && (t < h.t || key > h.key)) {
+      if (ok & ((t < h.t) | (key > h.key))) {
         h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
       }
     }
@@ -950,7 +949,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       }
       // t <= h.t here; an equal t replaces the hit only if it comes later in the reference's DFS
       // leaf order (the reference keeps the last of equal-t hits)
-      if (ok && (t < h.t || key > h.key)) {
+      if (ok & ((t < h.t) | (key > h.key))) {
         h.t = t; h.prim = pi; h.key = key; h.b1 = b1; h.b2 = b2;
       }
     }
@@ -963,16 +962,16 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       while (ref >= 0) {
         BDPT_LANE_PROF(c, LP_CNODE);
         ref = node_step<K, LM, kClosestOrd>(S, r, ref, tmin, h.t, stk, c);
-        if (ref < 0 && ref != kTravDone && pend == 0) {
+        if ((ref < 0) & (ref != kTravDone) & (pend == 0)) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-        if (wave_count(pend == 0 && ref >= 0) == 0) break;
+        if (wave_count((pend == 0) & (ref >= 0)) == 0) break;
       }
       while (pend != 0) {
         test_leaf(pend);
         pend = 0;
-        if (ref < 0 && ref != kTravDone) {
+        if ((ref < 0) & (ref != kTravDone)) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
@@ -1099,16 +1098,16 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       while (ref >= 0) {
         BDPT_LANE_PROF(c, LP_ANODE);
         ref = node_step<K, LM, kAnyOrd>(S, r, ref, tmin, tmax, stk, c);
-        if (ref < 0 && ref != kTravDone && pend == 0) {
+        if ((ref < 0) & (ref != kTravDone) & (pend == 0)) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
-        if (wave_count(pend == 0 && ref >= 0) == 0) break;
+        if (wave_count((pend == 0) & (ref >= 0)) == 0) break;
       }
       while (pend != 0) {
         if (test_leaf(pend)) return true;
         pend = 0;
-        if (ref < 0 && ref != kTravDone) {
+        if ((ref < 0) & (ref != kTravDone)) {
           pend = ref;
           if (!stk.pop(ref)) ref = kTravDone;
         }
