@@ -636,6 +636,20 @@ template <int LM>
 BDPT_HD float4 ld_geom(const SceneView& S, int k) {
   return LM == 1 || LM == 3 ? ld_lds4(S.lgeom + k) : ld_glb4(S.geom + k);
 }
+// primitive pi's whole record (3 float4). From HBM: the array's base as the scalar part of the
+// address, a 32-bit per-lane offset, the rows' 0 / 16 / 32 in the immediate field.
+template <int LM>
+BDPT_HD void ld_rec3(const SceneView& S, int pi, float4& a0, float4& a1, float4& a2) {
+  if (LM == 1 || LM == 3) {
+    a0 = ld_lds4(S.lgeom + 3 * pi); a1 = ld_lds4(S.lgeom + 3 * pi + 1); a2 = ld_lds4(S.lgeom + 3 * pi + 2);
+  } else {
+    const char* b = (const char*)S.geom;
+    const size_t o = (size_t)((uint32_t)pi * 48u);
+    a0 = ld_glb4((const float4*)(b + o));
+    a1 = ld_glb4((const float4*)(b + 16 + o));
+    a2 = ld_glb4((const float4*)(b + 32 + o));
+  }
+}
 BDPT_HD int ld_lds_i(const int* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return *(const __attribute__((address_space(3))) int*)p;
@@ -883,12 +897,12 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   int li = 0;
   if (LM == 3 && S.fn > 0) {
     // the flat list as one run of primitives, the next record's loads issued before this test
-    float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
+    float4 a0, a1, a2;
+    ld_rec3<LM>(S, 0, a0, a1, a2);
     for (int pi = 0; pi < S.fn; pi++) {
       BDPT_LANE_PROF(c, LP_CPRIM);
       const float4 g0 = a0, g1 = a1, g2 = a2;
-      const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
-      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+      ld_rec3<LM>(S, pi + 1 < S.fn ? pi + 1 : pi, a0, a1, a2);
       float t, b1 = 0, b2 = 0;
       bool ok;
       int key;
@@ -913,7 +927,7 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
   auto test_leaf = [&](int lf) {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM)) {
-      a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
+      ld_rec3<LM>(S, st, a0, a1, a2);
     }
     for (int k = 0; k < cnt; k++) {
       BDPT_LANE_PROF(c, LP_CPRIM);
@@ -922,10 +936,9 @@ BDPT_HD bool trace_closest(const SceneView& S, f3 o, f3 d, float tmin, float tma
       bool ok;
       int key;
       if constexpr (leaf_prefetch(LM)) {
-        // this record was loaded one test ahead; issue the next one's loads before testing it
+        // this record was loaded one test ahead; issue the next one's loads (if any) before testing it
         const float4 g0 = a0, g1 = a1, g2 = a2;
-        const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
-        a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+        if (k + 1 < cnt) ld_rec3<LM>(S, pi + 1, a0, a1, a2);
         if ((sm >> k) & 1) {
           c.sphs++;
           ok = sph_test(g0, o, d, tmin, h.t, &t);
@@ -1036,12 +1049,12 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
 #endif
   int li = 0;
   if (LM == 3 && S.fn > 0) {
-    float4 a0 = ld_geom<LM>(S, 0), a1 = ld_geom<LM>(S, 1), a2 = ld_geom<LM>(S, 2);
+    float4 a0, a1, a2;
+    ld_rec3<LM>(S, 0, a0, a1, a2);
     for (int pi = 0; pi < S.fn; pi++) {
       BDPT_LANE_PROF(c, LP_APRIM);
       const float4 g0 = a0, g1 = a1, g2 = a2;
-      const int nx = 3 * (pi + 1 < S.fn ? pi + 1 : pi);
-      a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+      ld_rec3<LM>(S, pi + 1 < S.fn ? pi + 1 : pi, a0, a1, a2);
       float t, b1, b2;
       bool ok;
       if ((S.fsph >> pi) & 1u) {
@@ -1060,7 +1073,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
   auto test_leaf = [&](int lf) -> bool {
     const int st = leaf_start(lf), cnt = leaf_count(lf), sm = leaf_sph_mask(lf);
     if constexpr (leaf_prefetch(LM)) {
-      a0 = ld_geom<LM>(S, 3 * st); a1 = ld_geom<LM>(S, 3 * st + 1); a2 = ld_geom<LM>(S, 3 * st + 2);
+      ld_rec3<LM>(S, st, a0, a1, a2);
     }
     for (int k = 0; k < cnt; k++) {
       BDPT_LANE_PROF(c, LP_APRIM);
@@ -1069,8 +1082,7 @@ BDPT_HD bool trace_any(const SceneView& S, f3 o, f3 d, float tmin, float tmax, C
       bool ok;
       if constexpr (leaf_prefetch(LM)) {
         const float4 g0 = a0, g1 = a1, g2 = a2;
-        const int nx = 3 * (k + 1 < cnt ? pi + 1 : pi);
-        a0 = ld_geom<LM>(S, nx); a1 = ld_geom<LM>(S, nx + 1); a2 = ld_geom<LM>(S, nx + 2);
+        if (k + 1 < cnt) ld_rec3<LM>(S, pi + 1, a0, a1, a2);
         if ((sm >> k) & 1) {
           c.sphs++;
           ok = sph_test(g0, o, d, tmin, tmax, &t);
