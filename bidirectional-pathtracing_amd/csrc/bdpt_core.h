@@ -416,9 +416,16 @@ constexpr int kStackMax = 64;
 // with 8 LDS slots behind them (kLdsStack): walk / connection 2/2, 3/3, 2/4, 4/2 lose 0.6 .. 1.7 %
 // on the north star (profiles/r04k_ab_regstack.log). Round 5, with the LDS slots: 0 / 0 and 0 / 4
 // -0.5 % on the north star, 4 / 0 +-0.2 %; with the tree in HBM (no LDS slots) 0 / 0 -10 %, and on
-// CBgems (LM 1) -2 % (profiles/r05y_ab_regstack.log).
-constexpr int kWalkStack = 4;
-constexpr int kConnStack = 4;
+// CBgems (LM 1) -2 % (profiles/r05y_ab_regstack.log). Round 6, after the leaner node step: 3 / 3,
+// 2 / 2, 4 / 2, 2 / 4 lose 0.4 .. 1 % on the north star, up to 2 % on CBgems (r06z3_ab_regstack.log).
+#ifndef BDPT_WALK_STACK
+#define BDPT_WALK_STACK 4
+#endif
+#ifndef BDPT_CONN_STACK
+#define BDPT_CONN_STACK 4
+#endif
+constexpr int kWalkStack = BDPT_WALK_STACK;   // variant builds may override (-DBDPT_WALK_STACK=...)
+constexpr int kConnStack = BDPT_CONN_STACK;
 // Children per BVH node: 2 (64-B nodes) or 4 (128-B nodes: half the dependent node fetches per
 // ray, four independent slab tests per fetch). The host emits both trees over the same leaves;
 // a kernel traverses the one its LDS mode selects: scenes fetched from HBM (LM 0, LM 2's nodes below
