@@ -671,6 +671,8 @@ BDPT_HD int ld_lds_i(const int* p) {
 // a global load) plus a 32-bit per-lane byte offset, the row's constant part in the immediate field:
 // against a 64-bit address per row (round 6, profiles/r06qrs_ab_lean_node.log) the per-ray offsets
 // take 6 VGPRs instead of 12 and the north-star kernel's static scratch instructions fall 236 -> 187.
+// 32-bit offsets suffice: a scene holds < 2^24 primitive references (bdpt_scene.cpp), so < 2^25 binary
+// and fewer 4-wide nodes, 128 ref + 112 < 2^32; the records (ld_rec3) are < 48 * 2^24 bytes.
 BDPT_HD void ld_node4_oct_glb(const float4* nodes, int ref, const RayInv& r, float4* v) {
   const char* b = (const char*)nodes;
   const uint32_t o = (uint32_t)ref * 128u;
