@@ -868,9 +868,16 @@ BDPT_HD int node_step(const SceneView& S, const RayInv& r, int ref, float tmin, 
       int nx;
       return stk.pop(nx) ? nx : kTravDone;
     }
-    if (k3 < INFINITY) stk.push(r3);
-    if (k2 < INFINITY) stk.push(r2);
-    if (k1 < INFINITY) stk.push(r1);
+    // the keys are sorted, so a later child is hit only if the earlier ones are: nested, a wave skips
+    // the deeper pushes unless one of its lanes has that many hit children (against three flat
+    // conditional pushes: north star +1.4 %, C5-shaped +1.8 %, profiles/r06z6_ab_push_nest.log)
+    if (k1 < INFINITY) {
+      if (k2 < INFINITY) {
+        if (k3 < INFINITY) stk.push(r3);
+        stk.push(r2);
+      }
+      stk.push(r1);
+    }
     return r0;
   }
 }
